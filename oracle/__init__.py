@@ -1,0 +1,4 @@
+"""ORACLE — test infrastructure only (CPU restatement of the reference's hot path).
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
