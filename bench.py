@@ -1,0 +1,214 @@
+"""Benchmark: LRS-PnP outer ADMM iterations/sec on the BASELINE.json configs[1] workload.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cube 200x200x198] [--bb 8] [--nit 80]
+
+One "step" = one outer ADMM iteration of main_LRS_PnP.py (:250-366) over a whole synthetic
+200x200x198 cube: im2col of X + L1/mu1, fused masked ISTA + PnP-NLM prox over all 125,000 8x8
+blocks (Nit = 80, K = 256), SVT low-rank prox (concurrent stream), col2im + X + dual updates.
+Inputs are resident in HBM before the timed region.
+
+Multi-GPU (torchrun): one independent cube per rank (seed = rank), no data-path collective
+(weak scaling); barrier + synchronize around the K timed steps, MAX over ranks;
+value = (ranks * K) / max_time.
+
+Rank 0 prints one JSON line, including
+  roofline    : the dominant kernel (lrs_ista_f32 / k_ista) — algorithmic MFMA FLOPs per launch
+                (Nit*nb*4*n*K + nb*2*n*K) / mean launch time (HIP events on its stream), vs the
+                157.3 TFLOP/s fp32 MFMA peak; `traffic` from profiles/ PMC summary when present;
+  cpu_baseline: the oracle (C restatement + numpy alpha/SVT, OpenMP) timed on a bounded sample
+                of the same workload on this host (N = 1, rank 0 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "lrs-pnp-dip_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cube", default="200x200x198")
+    ap.add_argument("--bb", type=int, default=8)
+    ap.add_argument("--nit", type=int, default=80)
+    ap.add_argument("--K", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def make_problem(H, W, B, bb, K, seed):
+    from lrspnp.data import load_fixture, mask_matrix, synthetic_cube, synthetic_dictionary, unfold
+    base = load_fixture("data_img5.npz")["lrs_mask"]
+    obs, clean, mask = synthetic_cube(H, W, B, seed=seed, base_mask=base)
+    return unfold(obs), mask_matrix(mask, B), synthetic_dictionary(bb * bb, K, 0), clean
+
+
+def cpu_baseline(Y, M, D, bb, nit, budget_s):
+    """Oracle timed on a bounded sample of the same workload (host cores)."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    P, B = Y.shape
+    rows, cols = O.block_grid(P, B, bb, bb)
+    nb = rows.size
+    rng = np.random.default_rng(0)
+    # per-block cost: alpha (numpy float32 SVD of the pruned dictionary, as ista() does per call)
+    # + the C ISTA (GEMVs + NLM) — grow the sample until the budget is used
+    blocks = O.im2col(Y, bb, rows, cols)
+    obs = (blocks != 0).astype(np.uint8)
+    done, t_ista, t_alpha = 0, 0.0, 0.0
+    batch = 256
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < budget_s * 0.7 and done < nb:
+        idx = rng.choice(nb, batch, replace=False)
+        t0 = time.perf_counter()
+        al = np.empty(batch, np.float32)
+        th = np.empty(batch, np.float64)
+        for k, j in enumerate(idx):
+            al[k], th[k] = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, "spec2")
+        t1 = time.perf_counter()
+        O.ista_batch(blocks[idx], obs[idx], D, al, th, nit)
+        t2 = time.perf_counter()
+        t_alpha += t1 - t0
+        t_ista += t2 - t1
+        done += batch
+    per_block = (t_alpha + t_ista) / done
+    t0 = time.perf_counter()
+    U = O.svt(Y, 1 / 0.9)                                   # the reference's float32 LAPACK SVT
+    t_svt = time.perf_counter() - t0
+    X = Y.copy()
+    PHI = np.zeros((nb, bb * bb), np.float32)
+    t0 = time.perf_counter()
+    O.lib().oracle_admm_update(P, B, bb, nb, rows, cols, PHI, Y, M, U, X, X, 0.5, np.float32(0.15),
+                               np.float32(0.9), X.copy(), X.copy(), X.copy(), None, None)
+    t_admm = time.perf_counter() - t0
+    t_iter = per_block * nb + t_svt + t_admm
+    return {"value": 1.0 / t_iter, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+            "sample": f"{done} of {nb} blocks (alpha+ISTA, Nit={nit}) extrapolated x{nb / done:.1f}, "
+                      f"+ full SVT ({t_svt:.2f}s) + full ADMM update ({t_admm:.3f}s); "
+                      f"est. {t_iter:.1f}s per outer iteration"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    from lrspnp import LrsPnP, LrsPnPConfig, ops
+    from lrspnp.metrics import mpsnr
+
+    H, W, B = (int(v) for v in args.cube.split("x"))
+    Y, M, D, clean = make_problem(H, W, B, args.bb, args.K, seed=rank)
+    cfg = LrsPnPConfig(bb=args.bb, sliding=args.bb, Nit=args.nit, variant="spec2")
+    t0 = time.perf_counter()
+    s = LrsPnP(Y, M, D, cfg)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
+    clean_d = torch.from_numpy(clean).cuda()
+    mp0 = mpsnr(s.X, clean_d)
+
+    # dominant-kernel timing: HIP events on the stream the ISTA kernel is launched on
+    main_stream = torch.cuda.current_stream()
+    ev = []
+    orig_ista = ops.ista
+
+    def timed_ista(*a, **k):
+        st = k.get("stream") or torch.cuda.current_stream()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        out = orig_ista(*a, **k)
+        e1.record(st)
+        ev.append((e0, e1))
+        return out
+
+    import lrspnp.solver as solver_mod
+    solver_mod.ops.ista = timed_ista
+    for _ in range(args.warmup):
+        s.step()
+    torch.cuda.synchronize()
+    ev.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    solver_mod.ops.ista = orig_ista
+    ista_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    mp1 = mpsnr(s.X, clean_d)
+
+    n, K, nb = args.bb * args.bb, args.K, s.nb
+    flops = args.nit * nb * 4 * n * K + nb * 2 * n * K
+    achieved = flops / (ista_ms * 1e-3) / 1e12
+    traffic = None
+    prof = os.path.join(REPO, "profiles", "ista_pmc_traffic.json")
+    if os.path.exists(prof):
+        try:
+            traffic = json.load(open(prof)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": world * args.steps / elapsed,
+        "unit": "outer_iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (MFMA) + f64 (NLM prox, Gram/eig)",
+        "data": "synthetic (seeded low-rank cube per rank, tiled low_rank_sparsity_mask, seeded K=256 dictionary)",
+        "config": {"workload": f"LRS-PnP (no DIP) {args.cube} cube, {args.bb}x{args.bb} blocks, K={K}, "
+                               f"Nit={args.nit} inner ISTA, SVT low-rank prox (BASELINE configs[1])",
+                   "blocks": nb, "parallelism": f"{world} independent cube(s), one per GPU"},
+        "roofline": {"bound": "mfma", "kernel": "k_ista (lrs_ista_f32)", "achieved": achieved,
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                     "traffic": traffic, "flops_per_launch": flops, "ms_per_launch": ista_ms},
+        "setup_s": setup_s,
+        "mpsnr": {"input": mp0, "after_steps": mp1, "steps_run": args.warmup + args.steps},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(Y, M, D, args.bb, args.nit, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+"""ctypes binding of liblrspnp_hip.so (include/lrspnp.h).
+
+The product path has no CPU fallback: if the library is missing, fails to load, or the device is
+not gfx950, every op raises ``LrsError`` instead of computing anything elsewhere.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblrspnp_hip.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+LRS_OK = 0
+LRS_E = {-1: "LRS_E_INVALID", -2: "LRS_E_UNSUPPORTED", -3: "LRS_E_WORKSPACE", -4: "LRS_E_NODEVICE"}
+
+ALPHA_SPEC2, ALPHA_FRO4, ALPHA_SOFT = 0, 1, 2
+PROX_NLM, PROX_SOFT = 0, 1
+
+
+class LrsError(RuntimeError):
+    pass
+
+
+_lib = None
+_device_checked = False
+
+
+def build(force: bool = False) -> str:
+    """Compile csrc/ for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    import subprocess
+
+    if force:
+        subprocess.check_call(["make", "-s", "-C", CSRC, "clean"])
+    subprocess.check_call(["make", "-s", "-j8", "-C", CSRC])
+    return LIB_PATH
+
+
+def _declare(L):
+    c = ctypes
+    vp, i64, i32, f32, f64, sz = c.c_void_p, c.c_int64, c.c_int, c.c_float, c.c_double, c.c_size_t
+    i32p = c.POINTER(c.c_int32)
+    sig = {
+        "lrs_version": (c.c_char_p, []),
+        "lrs_check_device": (i32, []),
+        "lrs_nlm_col_f32": (i32, [vp, i64, vp, i64, i64, i64, f64, vp, i32, i32, vp]),
+        "lrs_block_count": (i64, [i64, i64, i64, i64]),
+        "lrs_block_grid": (i32, [i64, i64, i64, i64, i32p, i32p, i64]),
+        "lrs_cover_ranges": (i32, [i64, i64, i32p, i64, i32p, i32p]),
+        "lrs_im2col_f32": (i32, [vp, vp, f32, i64, i64, i64, vp, vp, i64, i64, vp, vp, vp]),
+        "lrs_ista_alpha_workspace": (sz, [i64, i64, i64]),
+        "lrs_ista_alpha_f32": (i32, [vp, i64, i64, vp, i64, i64, i32, f32, vp, vp, vp, sz, vp]),
+        "lrs_ista_f32": (i32, [vp, vp, vp, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp, vp]),
+        "lrs_svt_workspace": (sz, [i64, i64]),
+        "lrs_svt_f32": (i32, [vp, vp, f32, i64, i64, f64, vp, vp, i32, vp, sz, vp]),
+        "lrs_admm_update_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, i64, vp, vp,
+                                      vp, vp, f32, f32, f32, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+def lib():
+    """The loaded library (host-side entry points usable without a GPU)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LrsError(f"{LIB_PATH} not built: run __graft_entry__.build() (make -C {CSRC})")
+        try:
+            _lib = _declare(ctypes.CDLL(LIB_PATH))
+        except OSError as e:  # pragma: no cover - environment problem
+            raise LrsError(f"cannot load {LIB_PATH}: {e}") from e
+    return _lib
+
+
+def device_lib():
+    """The library, after checking that the current device is a gfx950 (MI355X)."""
+    global _device_checked
+    L = lib()
+    if not _device_checked:
+        import torch
+
+        if not torch.cuda.is_available():
+            raise LrsError("no ROCm GPU visible: lrspnp has no CPU fallback")
+        rc = L.lrs_check_device()
+        if rc != LRS_OK:
+            raise LrsError(f"lrs_check_device: {LRS_E.get(rc, rc)} (need gfx950)")
+        _device_checked = True
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != LRS_OK:
+        raise LrsError(f"{what} failed: {LRS_E.get(rc, f'hipError {rc}')}")

@@ -1,0 +1,166 @@
+"""Tensor-level wrappers over the C ABI (include/lrspnp.h).
+
+torch is only plumbing here: device memory, the current HIP stream, dtype/shape checks.  Every
+arithmetic step runs in liblrspnp_hip.so; nothing falls back to torch/numpy compute.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import (ALPHA_FRO4, ALPHA_SOFT, ALPHA_SPEC2, PROX_NLM, PROX_SOFT, LrsError, check,
+                   device_lib, lib)
+
+__all__ = ["nlm_col", "block_grid", "cover_ranges", "im2col", "ista_alpha", "ista", "svt_workspace",
+           "svt", "admm_update", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT"]
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _s(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _dev(t, dtype, name):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise LrsError(f"{name} must be a CUDA(ROCm) tensor")
+    if t.dtype != dtype:
+        raise LrsError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise LrsError(f"{name} must be contiguous")
+    return t
+
+
+# ---------------------------------------------------------------------------------------------
+def nlm_col(g: torch.Tensor, h, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """NLM prox of every row of g (nvec, K): skimage denoise_nl_means(g_v[:,None], h, fast_mode=True,
+    patch_size=3, patch_distance=3) per vector.  h: float or a float64 device tensor (nvec,)."""
+    L = device_lib()
+    g = _dev(g, torch.float32, "g")
+    if g.dim() == 1:
+        g2 = g.view(1, -1)
+    else:
+        g2 = g
+    nvec, K = g2.shape
+    o = torch.empty_like(g2) if out is None else _dev(out, torch.float32, "out").view(nvec, K)
+    hv = None
+    hs = 0.0
+    if isinstance(h, torch.Tensor):
+        hv = _dev(h, torch.float64, "h")
+    else:
+        hs = float(h)
+    check(L.lrs_nlm_col_f32(_p(g2), K, _p(o), K, K, nvec, hs, _p(hv), 3, 3, _s(stream)), "lrs_nlm_col_f32")
+    return o.view_as(g)
+
+
+def block_grid(P: int, B: int, bb: int, sliding: int):
+    """get_image_block corners (host int32 arrays), in the reference's order."""
+    L = lib()
+    nb = L.lrs_block_count(P, B, bb, sliding)
+    if nb < 0:
+        check(int(nb), "lrs_block_count")
+    rows = np.empty(nb, np.int32)
+    cols = np.empty(nb, np.int32)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    check(L.lrs_block_grid(P, B, bb, sliding, rows.ctypes.data_as(i32p), cols.ctypes.data_as(i32p), nb),
+          "lrs_block_grid")
+    return rows, cols
+
+
+def cover_ranges(extent: int, bb: int, starts: np.ndarray):
+    L = lib()
+    starts = np.ascontiguousarray(starts, np.int32)
+    lo = np.empty(extent, np.int32)
+    hi = np.empty(extent, np.int32)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    check(L.lrs_cover_ranges(extent, bb, starts.ctypes.data_as(i32p), starts.size, lo.ctypes.data_as(i32p),
+                             hi.ctypes.data_as(i32p)), "lrs_cover_ranges")
+    return lo, hi
+
+
+def im2col(X, Lm, mu: float, bb: int, rows_d, cols_d, n_pad: int, Yb=None, obs=None, want_obs=False,
+           stream=None):
+    """Yb[j] = block j of (X + Lm/mu) flattened F-order (get_image_block), zero-padded to n_pad."""
+    L = device_lib()
+    X = _dev(X, torch.float32, "X")
+    if Lm is not None:
+        _dev(Lm, torch.float32, "L")
+    P, B = X.shape
+    nb = rows_d.numel()
+    if Yb is None:
+        Yb = torch.empty((nb, n_pad), dtype=torch.float32, device=X.device)
+    if want_obs and obs is None:
+        obs = torch.empty((nb, n_pad), dtype=torch.uint8, device=X.device)
+    check(L.lrs_im2col_f32(_p(X), _p(Lm), float(mu), P, B, bb, _p(rows_d), _p(cols_d), nb, n_pad, _p(Yb),
+                           _p(obs) if want_obs else None, _s(stream)), "lrs_im2col_f32")
+    return (Yb, obs) if want_obs else Yb
+
+
+def ista_alpha(D, obs_pat, n: int, mode: int, lambda_ista: float, stream=None):
+    L = device_lib()
+    D = _dev(D, torch.float32, "D")
+    obs_pat = _dev(obs_pat, torch.uint8, "obs_pat")
+    nD, K = D.shape
+    npat, n_pad = obs_pat.shape
+    alpha = torch.empty(npat, dtype=torch.float32, device=D.device)
+    thr = torch.empty(npat, dtype=torch.float64, device=D.device)
+    wsb = L.lrs_ista_alpha_workspace(n, K, npat)
+    ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=D.device)
+    check(L.lrs_ista_alpha_f32(_p(D), n, K, _p(obs_pat), npat, n_pad, mode, float(lambda_ista), _p(alpha),
+                               _p(thr), _p(ws), ws.numel(), _s(stream)), "lrs_ista_alpha_f32")
+    return alpha, thr
+
+
+def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=None, coefs=None,
+         want_coefs=False, stream=None):
+    """Masked ISTA + prox over all blocks; returns phi (nb, n_pad) [, coefs (nb, K)]."""
+    L = device_lib()
+    _dev(Yb, torch.float32, "Yb")
+    _dev(obs, torch.uint8, "obs")
+    _dev(D, torch.float32, "D")
+    _dev(alpha, torch.float32, "alpha")
+    _dev(thr, torch.float64, "thr")
+    nb, n_pad = Yb.shape
+    K = D.shape[1]
+    if phi is None:
+        phi = torch.empty((nb, n_pad), dtype=torch.float32, device=Yb.device)
+    if want_coefs and coefs is None:
+        coefs = torch.empty((nb, K), dtype=torch.float32, device=Yb.device)
+    check(L.lrs_ista_f32(_p(Yb), _p(obs), _p(D), n, n_pad, K, nb, _p(alpha), _p(thr), int(Nit), int(prox),
+                         _p(coefs) if want_coefs else None, _p(phi), _s(stream)), "lrs_ista_f32")
+    return (phi, coefs) if want_coefs else phi
+
+
+def svt_workspace(P: int, B: int, device) -> torch.Tensor:
+    n = int(lib().lrs_svt_workspace(P, B))
+    return torch.zeros(n, dtype=torch.uint8, device=device)
+
+
+def svt(X, L2, c2: float, tau: float, ws, U=None, s_out=None, warm=False, stream=None):
+    """U = SVT(X + c2*L2, tau) (main_LRS_PnP.py:118-124)."""
+    L = device_lib()
+    _dev(X, torch.float32, "X")
+    if L2 is not None:
+        _dev(L2, torch.float32, "L2")
+    P, B = X.shape
+    if U is None:
+        U = torch.empty_like(X)
+    check(L.lrs_svt_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out), int(bool(warm)), _p(ws),
+                        ws.numel(), _s(stream)), "lrs_svt_f32")
+    return U
+
+
+def admm_update(X, L1, L2, Y, M, U, phi, bb, grid, gamma, mu1, mu2, norms=None, imout=None, stream=None):
+    """In-place col2im + X update + dual updates (main_LRS_PnP.py:324-362)."""
+    L = device_lib()
+    P, B = X.shape
+    n_pad = phi.shape[1]
+    check(L.lrs_admm_update_f32(_p(X), _p(L1), _p(L2), _p(Y), _p(M), _p(U), _p(phi), P, B, bb, n_pad,
+                                _p(grid["rstarts"]), _p(grid["cstarts"]), grid["nbr"], _p(grid["rlo"]),
+                                _p(grid["rhi"]), _p(grid["clo"]), _p(grid["chi"]), float(gamma), float(mu1),
+                                float(mu2), _p(norms), _p(imout), _s(stream)), "lrs_admm_update_f32")

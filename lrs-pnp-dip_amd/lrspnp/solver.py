@@ -1,0 +1,139 @@
+"""Batched LRS-PnP ADMM outer loop on one MI355X (host orchestration only).
+
+Mirrors the module-level loop of main_LRS_PnP.py:244-366 (SVT low-rank prox) with the DIP
+variants' ISTA rule selectable (…1-LiP.py:185-198).  One `step()` = one outer ADMM iteration:
+
+    main stream : im2col(X + L1/mu1) -> fused masked ISTA + PnP prox (all blocks) -> Phi
+    lowrank str.: SVT(X + L2/mu2, 1/mu2) -> U            (runs concurrently with the ISTA)
+    main stream : col2im + closed-form X + dual updates + ||delta||^2   (waits for both)
+
+No per-block Python, no host synchronisation inside `step()`.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import ops
+from ._lib import LrsError
+
+
+@dataclass
+class LrsPnPConfig:
+    """The knob table of SURVEY.md §5 (main_LRS_PnP.py:218-238 defaults)."""
+    gamma: float = 0.5            # data fidelity                      main_LRS_PnP.py:218
+    mu1: float = 0.15             # sparsity penalty                   :221
+    mu2: float = 0.15 * 6         # low-rank penalty                   :222
+    lambda_ista: float = 0.1      # ISTA lambda                         :225
+    Nit: int = 80                 # inner ISTA iterations               :226
+    bb: int = 36                  # block size                          :237
+    sliding: int = 36             # slidingDis                          :238
+    variant: str = "spec2"        # 'spec2' (main), 'fro4' (DIP mains), 'soft' (ista.m)
+    svt_warm: bool = True         # warm-start the Jacobi eigensolver from the previous iteration
+
+    @staticmethod
+    def dip_1lip(**kw) -> "LrsPnPConfig":
+        """Parameters of main_LRS_PnP_DIP_1-LiP.py:316-333 (SVT stands in for the DIP prox)."""
+        base = dict(gamma=0.5, mu1=0.1, mu2=0.1, lambda_ista=0.1, Nit=100, bb=36, sliding=36, variant="fro4")
+        base.update(kw)
+        return LrsPnPConfig(**base)
+
+
+_ALPHA = {"spec2": ops.ALPHA_SPEC2, "fro4": ops.ALPHA_FRO4, "soft": ops.ALPHA_SOFT}
+
+
+class LrsPnP:
+    """LRS-PnP solver state on the current ROCm device.
+
+    Y: observed unfolded cube (P x B, zeros at missing entries), M: mask (P x B), D: n x K
+    dictionary with n = bb*bb.  All float32 (numpy or torch); copied to the device once.
+    """
+
+    def __init__(self, Y, M, D, cfg: LrsPnPConfig | None = None, device="cuda"):
+        self.cfg = cfg = cfg or LrsPnPConfig()
+        dev = torch.device(device)
+        f = lambda a: torch.as_tensor(np.asarray(a, np.float32) if not isinstance(a, torch.Tensor) else a,
+                                      dtype=torch.float32).to(dev).contiguous()
+        self.Y, self.M, self.D = f(Y), f(M), f(D)
+        self.P, self.B = self.Y.shape
+        n, self.K = self.D.shape
+        if n != cfg.bb * cfg.bb:
+            raise LrsError(f"dictionary has {n} rows, expected bb*bb = {cfg.bb * cfg.bb}")
+        self.n = n
+        self.n_pad = -(-n // 16) * 16
+        f32 = np.float32
+        self.gamma32, self.mu1_32, self.mu2_32 = f32(cfg.gamma), f32(cfg.mu1), f32(cfg.mu2)
+        self.c2 = f32(1 / cfg.mu2)                        # (1/mu_2)*lambda_2   main_LRS_PnP.py:315
+        self.tau = float(f32(1 / cfg.mu2))                # SVT threshold (float32 in numpy)
+        self.prox = ops.PROX_SOFT if cfg.variant == "soft" else ops.PROX_NLM
+
+        # ---- block grid (host bookkeeping) -------------------------------------------------
+        rows, cols = ops.block_grid(self.P, self.B, cfg.bb, cfg.sliding)
+        self.nb = rows.size
+        rstarts = np.unique(rows).astype(np.int32)
+        cstarts = np.unique(cols).astype(np.int32)
+        self.nbr = rstarts.size
+        assert np.array_equal(rows, np.tile(rstarts, cstarts.size))
+        assert np.array_equal(cols, np.repeat(cstarts, rstarts.size))
+        rlo, rhi = ops.cover_ranges(self.P, cfg.bb, rstarts)
+        clo, chi = ops.cover_ranges(self.B, cfg.bb, cstarts)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self.rows_d, self.cols_d = t(rows), t(cols)
+        self.grid = dict(rstarts=t(rstarts), cstarts=t(cstarts), nbr=self.nbr, rlo=t(rlo), rhi=t(rhi),
+                         clo=t(clo), chi=t(chi))
+
+        # ---- observation masks of blocks_copy (main_LRS_PnP.py:244,278) and alpha/h --------
+        _, obs = ops.im2col(self.Y, None, 1.0, cfg.bb, self.rows_d, self.cols_d, self.n_pad, want_obs=True)
+        self.obs = obs
+        packed = np.packbits(obs.cpu().numpy(), axis=1)
+        uniq, inv = np.unique(packed, axis=0, return_inverse=True)
+        self.npat = uniq.shape[0]
+        obs_pat = t(np.unpackbits(uniq, axis=1)[:, : self.n_pad].astype(np.uint8))
+        alpha_pat, thr_pat = ops.ista_alpha(self.D, obs_pat, n, _ALPHA[cfg.variant], cfg.lambda_ista)
+        inv_d = t(inv.reshape(-1).astype(np.int64))
+        self.alpha = alpha_pat.index_select(0, inv_d).contiguous()
+        self.thr = thr_pat.index_select(0, inv_d).contiguous()
+        self.alpha_pat, self.thr_pat, self.obs_pat = alpha_pat, thr_pat, obs_pat
+
+        # ---- state and buffers -------------------------------------------------------------
+        self.X = self.Y.clone()                           # X = Y_observed     main_LRS_PnP.py:229
+        self.L1 = torch.zeros_like(self.Y)
+        self.L2 = torch.zeros_like(self.Y)
+        self.U = torch.empty_like(self.Y)
+        self.Yb = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
+        self.phi = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
+        self.norms = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.svt_ws = ops.svt_workspace(self.P, self.B, dev)
+        self.lowrank_stream = torch.cuda.Stream(device=dev)
+        self.iteration = 0
+
+    # -----------------------------------------------------------------------------------------
+    def sparse_coding(self, stream=None, want_coefs=False):
+        """Yb = blocks of X + L1/mu1; Phi = D * ISTA-PnP(Yb) for every block."""
+        ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
+                   stream=stream)
+        return ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox,
+                        phi=self.phi, want_coefs=want_coefs, stream=stream)
+
+    def low_rank(self, stream=None, s_out=None):
+        warm = self.cfg.svt_warm and self.iteration > 0
+        return ops.svt(self.X, self.L2, self.c2, self.tau, self.svt_ws, U=self.U, s_out=s_out, warm=warm,
+                       stream=stream)
+
+    def step(self):
+        """One outer ADMM iteration (main_LRS_PnP.py:250-366), stream-ordered, no host sync."""
+        main = torch.cuda.current_stream()
+        lr = self.lowrank_stream
+        lr.wait_stream(main)
+        self.sparse_coding(stream=main)
+        self.low_rank(stream=lr)
+        main.wait_stream(lr)
+        ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
+                        self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)
+        self.iteration += 1
+
+    def convergence(self):
+        """state_convergence (main_LRS_PnP.py:23-25) of X, lambda_1, lambda_2 for the last step."""
+        return torch.log(torch.sqrt(self.norms)).cpu().tolist()

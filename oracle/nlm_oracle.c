@@ -125,9 +125,12 @@ int oracle_nlm_fast2d(const float *img, int H, int W, int C, int s, int d, doubl
  * Closed form for a (K,1) column, s = 3, d = 3.  With the image one column wide
  * all 11 padded columns are equal, the integral-image window degenerates to rows p..p+1 and the
  * 28 shifts fold into
- *     out[i] = (2(d+1) w0 v[p] + (2d+1) sum_t w(p,t) v[p+t]) / (2(d+1) w0 + (2d+1) sum_t w(p,t))
- * with D(p,t) = 2[(v[p]-v[p+t])^2 + (v[p+1]-v[p+1+t])^2] / (9 h^2), w = fast_exp(-D) unless
- * D > 5.  Accumulation order follows the shift loop (t_row ascending), all in double.
+ *     out[i] = (8 w0 v[p] + 7 sum_t w(p,t) v[p+t]) / (8 w0 + 7 sum_t w(p,t)),   t = +-1,+-2,+-3
+ * with D(p,t) = [(v[p]-v[p+t])^2 + (v[p+1]-v[p+1+t])^2] * (2 / (9 h^2)), w = fast_exp(-D) unless
+ * D > 5.  This is the CANONICAL evaluation order the HIP kernels reproduce bit-for-bit
+ * (csrc/lrs_nlm.h): sums in t = -3..3 order, fma for the weighted sums, one double division.
+ * Against skimage's integral-image loop it differs only through rounding of D and of the double
+ * accumulators (<= 1 ulp of the float32 output, ~1e-5 of elements; tests/test_oracle.py).
  * g: K floats with stride `ldg`; out: K floats with stride `ldo`.
  */
 void oracle_nlm_col(const float *g, long K, long ldg, double h, float *out, long ldo) {
@@ -135,27 +138,23 @@ void oracle_nlm_col(const float *g, long K, long ldg, double h, float *out, long
     const long n = K + 2 * pad;
     double *v = (double *)malloc(sizeof(double) * (size_t)n);
     for (long i = 0; i < n; ++i) v[i] = (double)g[reflect_idx((int)(i - pad), (int)K) * ldg];
-    const double h2s2 = 9.0 * h * h;
-    const double w0 = fast_exp(-0.0);
+    const double inv2 = 2.0 / ((h * h) * 9.0);
+    const double c0 = 8.0 * fast_exp(-0.0);
     for (long i = 0; i < K; ++i) {
         long p = i + pad;
-        double num = 0.0, den = 0.0;
+        double sw = 0.0, swv = 0.0;
         for (int t = -d; t <= d; ++t) {
-            double w, val;
-            if (t == 0) {
-                w = w0; val = v[p];
-                num += (2.0 * (d + 1)) * w * val;
-                den += (2.0 * (d + 1)) * w;
-                continue;
-            }
+            if (t == 0) continue;
             double a = v[p] - v[p + t], b = v[p + 1] - v[p + 1 + t];
-            double D = 2.0 * (a * a + b * b) / h2s2;
+            double aa = a * a, bb = b * b;
+            double D = (aa + bb) * inv2;
             if (D > NLM_DISTANCE_CUTOFF) continue;
-            w = fast_exp(-D);
-            val = v[p + t];
-            num += (2.0 * d + 1.0) * w * val;
-            den += (2.0 * d + 1.0) * w;
+            double w = fast_exp(-D);
+            sw = sw + w;
+            swv = fma(w, v[p + t], swv);
         }
+        double num = fma(7.0, swv, c0 * v[p]);
+        double den = fma(7.0, sw, c0);
         out[i * ldo] = (float)(num / den);
     }
     free(v);

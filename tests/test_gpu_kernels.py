@@ -1,0 +1,223 @@
+"""Parity of the HIP kernels (through the C ABI) against the oracle, on a real MI355X.
+
+Tolerances (written here, per kernel):
+  * NLM prox kernel         : bit-exact vs the oracle's canonical closed form; <= 1 ulp vs skimage.
+  * fused ISTA (coefs, Phi) : 1e-5 relative L2 per block vs the oracle (MFMA fp32 products sum in
+                              a different order than the oracle's fp64-accumulated GEMVs).
+  * alpha (||H||_2^2)       : 2 ulp of float32 vs numpy's float32 SVD; fro4 1e-6 relative.
+  * SVT                     : 1e-5 relative L2 vs numpy float32 SVD (the reference's call).
+  * ADMM update             : bit-exact vs the oracle (same float32 operation order).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lrspnp import ops as _ops
+    return _ops
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def _split(flat, sizes):
+    out, o = [], 0
+    for s in sizes:
+        out.append(flat[o:o + s]); o += s
+    return out
+
+
+# ------------------------------------------------------------------------------------------ NLM
+def test_nlm_kernel_bitexact_vs_oracle(ops):
+    rng = np.random.default_rng(0)
+    for K in (1, 5, 8, 17, 64, 256, 1296):
+        for h in (1e-5, 4.9e-5, 3.2e-3, 0.05, 0.7):
+            for scale in (1e-4, 1e-2, 1.0):
+                g = (rng.standard_normal((7, K)) * scale).astype(np.float32)
+                got = ops.nlm_col(torch.from_numpy(g).cuda(), h).cpu().numpy()
+                for v in range(g.shape[0]):
+                    ref = O.nlm_col(g[v], h)
+                    assert np.array_equal(got[v].view(np.uint32), ref.view(np.uint32)), (K, h, scale, v)
+
+
+def test_nlm_kernel_vs_skimage_golden(ops, golden):
+    z = golden("nlm_golden.npz")
+    tot = bad = 0
+    for g, h, ref in zip(_split(z["col_in"], z["col_K"]), z["col_h"], _split(z["col_out"], z["col_K"])):
+        got = ops.nlm_col(torch.from_numpy(g).cuda(), float(h)).cpu().numpy()
+        d = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+        assert d.max() <= 1
+        tot += g.size; bad += int((d != 0).sum())
+    assert bad <= max(1, tot // 10000)
+
+
+def test_nlm_kernel_per_vector_h(ops):
+    rng = np.random.default_rng(1)
+    g = (rng.standard_normal((9, 256)) * 1e-3).astype(np.float32)
+    hs = np.geomspace(1e-5, 1e-1, 9)
+    got = ops.nlm_col(torch.from_numpy(g).cuda(), torch.from_numpy(hs).cuda()).cpu().numpy()
+    for v in range(9):
+        assert np.array_equal(got[v], O.nlm_col(g[v], hs[v]))
+
+
+# ------------------------------------------------------------------------------------------ ISTA
+def _rand_blocks(rng, nb, n, miss_frac, scale=0.3):
+    Yb = (rng.standard_normal((nb, n)) * scale).astype(np.float32)
+    obs = (rng.random((nb, n)) > miss_frac).astype(np.uint8)
+    obs[0, :] = 1                                  # one fully observed block
+    if nb > 2:
+        obs[1, : n // 2] = 0                       # a heavily masked one
+    Yb[obs == 0] = 0.0
+    return Yb, obs
+
+
+@pytest.mark.parametrize("bb,nb,Nit,variant", [(8, 300, 80, "spec2"), (8, 129, 100, "fro4"),
+                                               (8, 64, 40, "soft"), (36, 20, 12, "fro4"),
+                                               (36, 9, 10, "spec2")])
+def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant):
+    from lrspnp.data import synthetic_dictionary
+    rng = np.random.default_rng(bb * 1000 + nb)
+    n = bb * bb
+    n_pad = -(-n // 16) * 16
+    D = synthetic_dictionary(n, 256, seed=3)
+    Yb, obs = _rand_blocks(rng, nb, n, 0.2)
+    alpha = np.empty(nb, np.float32); thr = np.empty(nb, np.float64)
+    for j in range(nb):
+        alpha[j], thr[j] = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, variant)
+    prox = O.PROX_SOFT if variant == "soft" else O.PROX_NLM
+    Xo, PHIo = O.ista_batch(Yb, obs, D, alpha, thr, Nit, prox)
+    pad = lambda a: np.pad(a, ((0, 0), (0, n_pad - n)))
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    phi, coefs = ops.ista(d(pad(Yb)), d(pad(obs)), d(D), n, d(alpha), d(thr), Nit, prox, want_coefs=True)
+    phi = phi.cpu().numpy()[:, :n]
+    coefs = coefs.cpu().numpy()
+    worst = max(rel(coefs[j], Xo[j]) for j in range(nb))
+    worst_phi = max(rel(phi[j], PHIo[j]) for j in range(nb))
+    assert worst < 1e-5, worst
+    assert worst_phi < 1e-5, worst_phi
+
+
+def test_ista_kernel_vs_reference_golden(ops, golden):
+    """Reference `ista` outputs (captured from the unmodified reference, gen_golden.py)."""
+    from lrspnp.data import synthetic_dictionary
+    z = golden("ista_golden.npz")
+    D = synthetic_dictionary(1296, 256, 0)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    for variant in ("spec2", "fro4"):
+        Y, obs = z[variant + "_y"], z[variant + "_obs"]
+        nb = Y.shape[0]
+        alpha = np.empty(nb, np.float32); thr = np.empty(nb, np.float64)
+        for j in range(nb):
+            alpha[j], thr[j] = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, variant)
+        phi, coefs = ops.ista(d(Y), d(obs), d(D), 1296, d(alpha), d(thr), int(z[variant + "_Nit"]), 0,
+                              want_coefs=True)
+        for j in range(nb):
+            assert rel(coefs.cpu().numpy()[j], z[variant + "_coefs"][j]) < 1e-5
+            assert rel(phi.cpu().numpy()[j], z[variant + "_phi"][j]) < 1e-5
+
+
+def test_ista_deterministic(ops):
+    from lrspnp.data import synthetic_dictionary
+    rng = np.random.default_rng(5)
+    D = synthetic_dictionary(64, 256, 0)
+    Yb, obs = _rand_blocks(rng, 1000, 64, 0.1)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    alpha = d(np.full(1000, 5.0, np.float32)); thr = d(np.full(1000, 1e-3))
+    a = ops.ista(d(Yb), d(obs), d(D), 64, alpha, thr, 20, 0)
+    b = ops.ista(d(Yb), d(obs), d(D), 64, alpha, thr, 20, 0)
+    assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------------------------------------ alpha
+@pytest.mark.parametrize("n,variant", [(64, "spec2"), (64, "fro4"), (64, "soft"), (1296, "spec2"),
+                                       (1296, "fro4")])
+def test_alpha_kernel_vs_numpy(ops, n, variant):
+    from lrspnp.data import synthetic_dictionary
+    rng = np.random.default_rng(n)
+    D = synthetic_dictionary(n, 256, 0)
+    n_pad = -(-n // 16) * 16
+    npat = 6
+    obs = (rng.random((npat, n)) > np.linspace(0.0, 0.8, npat)[:, None]).astype(np.uint8)
+    obs[0] = 1
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    mode = {"spec2": 0, "fro4": 1, "soft": 2}[variant]
+    a, t = ops.ista_alpha(d(D), d(np.pad(obs, ((0, 0), (0, n_pad - n)))), n, mode, 0.1)
+    a = a.cpu().numpy(); t = t.cpu().numpy()
+    for j in range(npat):
+        ra, rt = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, variant)
+        if variant == "fro4":
+            assert abs(a[j] - ra) <= 1e-6 * ra
+        else:
+            assert abs(int(a[j].view(np.int32)) - int(np.float32(ra).view(np.int32))) <= 2, (j, a[j], ra)
+        assert abs(t[j] - rt) <= 4e-7 * rt
+
+
+# ------------------------------------------------------------------------------------------ SVT
+@pytest.mark.parametrize("P,B,rank,noise", [(1296, 128, 8, 0.12), (4000, 198, 8, 0.02), (500, 60, 3, 0.002)])
+def test_svt_kernel_vs_numpy(ops, P, B, rank, noise):
+    rng = np.random.default_rng(P + B)
+    Z = (rng.random((P, rank)) @ rng.random((rank, B)) * 0.3 + noise * rng.standard_normal((P, B)))
+    X = Z.astype(np.float32)
+    L2 = (0.01 * rng.standard_normal((P, B))).astype(np.float32)
+    c2 = np.float32(1 / 0.9)
+    tau = float(np.float32(1 / 0.9))
+    ref = O.svt(X + c2 * L2, 1 / 0.9)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    ws = ops.svt_workspace(P, B, "cuda")
+    s = torch.empty(B, dtype=torch.float64, device="cuda")
+    U = ops.svt(d(X), d(L2), c2, tau, ws, s_out=s, warm=False).cpu().numpy()
+    assert rel(U, ref) < 1e-5
+    sref = np.linalg.svd((X + c2 * L2).astype(np.float64), compute_uv=False)
+    assert rel(s.cpu().numpy(), sref) < 1e-9
+    # warm start from the previous eigenvectors on a perturbed matrix
+    X2 = (X + 1e-3 * rng.standard_normal((P, B))).astype(np.float32)
+    U2 = ops.svt(d(X2), d(L2), c2, tau, ws, warm=True).cpu().numpy()
+    assert rel(U2, O.svt(X2 + c2 * L2, 1 / 0.9)) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------ ADMM
+def test_admm_update_bitexact_vs_oracle(ops):
+    rng = np.random.default_rng(11)
+    for (P, B, bb) in [(1296, 128, 36), (400, 30, 8), (103, 29, 7)]:
+        rows, cols = O.block_grid(P, B, bb, bb)
+        nb = rows.size
+        n = bb * bb
+        n_pad = -(-n // 16) * 16
+        mk = lambda *s: rng.standard_normal(s).astype(np.float32)
+        Y, U, L1, L2, X = mk(P, B), mk(P, B), mk(P, B), mk(P, B), mk(P, B)
+        M = (rng.random((P, B)) > 0.1).astype(np.float32)
+        PHI = mk(nb, n)
+        Xo, L1o, L2o, IMo = (np.empty_like(X) for _ in range(4))
+        import ctypes
+        O.lib().oracle_admm_update(P, B, bb, nb, rows, cols, PHI, Y, M, U, L1, L2, 0.5, np.float32(0.15),
+                                   np.float32(0.9), Xo, L1o, L2o, IMo.ctypes.data_as(ctypes.c_void_p), None)
+        from lrspnp import ops as lops
+        r, c = lops.block_grid(P, B, bb, bb)
+        rs, cs = np.unique(r), np.unique(c)
+        rlo, rhi = lops.cover_ranges(P, bb, rs)
+        clo, chi = lops.cover_ranges(B, bb, cs)
+        d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        grid = dict(rstarts=d(rs), cstarts=d(cs), nbr=rs.size, rlo=d(rlo), rhi=d(rhi), clo=d(clo), chi=d(chi))
+        Xd, L1d, L2d = d(X), d(L1), d(L2)
+        im = torch.empty_like(Xd)
+        norms = torch.zeros(3, dtype=torch.float64, device="cuda")
+        lops.admm_update(Xd, L1d, L2d, d(Y), d(M), d(U), d(np.pad(PHI, ((0, 0), (0, n_pad - n)))), bb, grid,
+                         np.float32(0.5), np.float32(0.15), np.float32(0.9), norms=norms, imout=im)
+        assert np.array_equal(im.cpu().numpy(), IMo)
+        assert np.array_equal(Xd.cpu().numpy(), Xo)
+        assert np.array_equal(L1d.cpu().numpy(), L1o)
+        assert np.array_equal(L2d.cpu().numpy(), L2o)
+        nref = [np.sum((Xo.astype(np.float64) - X) ** 2), np.sum((L1o.astype(np.float64) - L1) ** 2),
+                np.sum((L2o.astype(np.float64) - L2) ** 2)]
+        assert np.allclose(norms.cpu().numpy(), nref, rtol=1e-10)

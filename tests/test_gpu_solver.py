@@ -1,0 +1,113 @@
+"""End-to-end parity of the batched GPU solver.
+
+* native 36x36x128 data (img5 + fourth_mask, K=256 seed-0 dictionary): two outer iterations of the
+  unmodified main_LRS_PnP.py captured in tests/golden/lrs_pnp_2iter.npz.  Tolerance: 1e-5 relative
+  L2 on X / lambda_1 / lambda_2, MPSNR identical to 2 dp (BASELINE.json north_star).
+* BASELINE configs[1] shape (200x200x198, bb=8, nb=125000): size-independent properties — a sample
+  of blocks re-solved by the oracle, determinism, finiteness, convergence norms.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return True
+
+
+def test_two_outer_iterations_vs_reference(gpu, golden):
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.data import synthetic_dictionary, unfold, mask_matrix
+    from lrspnp.metrics import mpsnr
+    d = golden("data_img5.npz")
+    g = golden("lrs_pnp_2iter.npz")
+    Y = unfold(d["noisy_img5"][0])
+    M = mask_matrix(d["fourth_mask"], 128)
+    D = synthetic_dictionary(1296, 256, 0)
+    s = LrsPnP(Y, M, D, LrsPnPConfig(bb=36, sliding=36, Nit=80, variant="spec2"))
+    clean = torch.from_numpy(d["clean_img5"][0]).cuda()
+    s.step()
+    torch.cuda.synchronize()
+    assert rel(s.X.cpu().numpy(), g["it1_X"]) < 1e-5
+    assert rel(s.L1.cpu().numpy(), g["it1_L1"]) < 1e-5
+    assert rel(s.L2.cpu().numpy(), g["it1_L2"]) < 1e-5
+    assert rel(s.U.cpu().numpy(), g["it1_U"]) < 1e-5
+    assert rel(s.phi.cpu().numpy()[:, :1296], g["it1_PHI"]) < 1e-5
+    p1 = mpsnr(s.X, clean)
+    s.step()
+    torch.cuda.synchronize()
+    assert rel(s.X.cpu().numpy(), g["it2_X"]) < 1e-5
+    assert rel(s.L1.cpu().numpy(), g["it2_L1"]) < 1e-5
+    assert rel(s.L2.cpu().numpy(), g["it2_L2"]) < 1e-5
+    p2 = mpsnr(s.X, clean)
+    assert round(p1, 2) == round(float(g["mpsnr"][0]), 2)
+    assert round(p2, 2) == round(float(g["mpsnr"][1]), 2)
+
+
+def test_dip_variant_sparse_coding_matches_oracle(gpu, golden):
+    """ISTA rule of the DIP mains (alpha = 4||H||_F^2, h = T, Nit = 100) on the native data."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.data import synthetic_dictionary, unfold, mask_matrix
+    d = golden("data_img5.npz")
+    Y = unfold(d["noisy"][0])
+    M = mask_matrix(d["lrs_mask"], 128)
+    D = synthetic_dictionary(1296, 256, 0)
+    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_1lip())
+    phi = s.sparse_coding().cpu().numpy()[:, :1296]
+    o = O.LrsPnpOracle(Y, M, D, bb=36, sliding=36, gamma=0.5, mu1=0.1, mu2=0.1, Nit=100, variant="fro4")
+    blocks = O.im2col(o.X + o.L1 / np.float32(0.1), 36, o.rows, o.cols)
+    _, PHI = O.ista_batch(blocks, o.obs, D, o.alpha, o.thr, 100)
+    assert rel(phi, PHI) < 1e-5
+    assert np.allclose(s.alpha.cpu().numpy(), o.alpha, rtol=1e-6)
+
+
+def test_config2_shape_properties(gpu):
+    """200x200x198 cube, bb = 8 (125,000 blocks), Nit = 80: the bench workload."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.data import synthetic_cube, synthetic_dictionary, unfold, mask_matrix, load_fixture
+    base = load_fixture("data_img5.npz")["lrs_mask"]
+    obs, clean, mask = synthetic_cube(200, 200, 198, seed=0, base_mask=base)
+    Y, M = unfold(obs), mask_matrix(mask, 198)
+    D = synthetic_dictionary(64, 256, 0)
+    cfg = LrsPnPConfig(bb=8, sliding=8, Nit=80, variant="spec2")
+    s = LrsPnP(Y, M, D, cfg)
+    assert s.nb == 125000
+    s.step()
+    torch.cuda.synchronize()
+    X1 = s.X.clone()
+    assert torch.isfinite(X1).all()
+    # oracle re-solve of a sample of blocks (same inputs: first iteration, L1 = 0)
+    rng = np.random.default_rng(0)
+    sample = rng.choice(s.nb, 48, replace=False)
+    Yb = s.Yb.cpu().numpy()[sample]
+    ob = s.obs.cpu().numpy()[sample]
+    Xo, PHIo = O.ista_batch(Yb, ob, D, s.alpha.cpu().numpy()[sample], s.thr.cpu().numpy()[sample], 80)
+    phi = s.phi.cpu().numpy()[sample, :64]
+    for k in range(sample.size):
+        assert rel(phi[k], PHIo[k]) < 1e-5
+    # the alpha of every distinct observation pattern vs numpy's float32 SVD
+    pats = s.obs_pat.cpu().numpy()
+    ap = s.alpha_pat.cpu().numpy()
+    for k in range(min(pats.shape[0], 40)):
+        ra, _ = O.ista_alpha_h(D[pats[k, :64].astype(bool)], 0.1, "spec2")
+        assert abs(int(ap[k].view(np.int32)) - int(np.float32(ra).view(np.int32))) <= 2
+    # determinism: a fresh solver reproduces the iterate bit for bit
+    s2 = LrsPnP(Y, M, D, cfg)
+    s2.step()
+    torch.cuda.synchronize()
+    assert torch.equal(s2.X, X1)
+    nx, n1, n2 = s.norms.cpu().numpy()
+    assert np.isfinite([nx, n1, n2]).all() and nx > 0
