@@ -28,7 +28,7 @@ constexpr int kIstaThreads = kIstaWaves * kWave;
 constexpr int kStageRows = 64;
 
 template <int K>
-struct IstaSmem {
+struct alignas(16) IstaSmem {
     float DA[kStageRows][K + 4];  // [row][atom]; +4 keeps b128 rows aligned, spreads banks
     float DT[K][kStageRows + 4];  // [atom][row]
 };
@@ -177,7 +177,7 @@ __device__ __forceinline__ void nlm_prox_registers(const floatx4 (&G)[K / 16], f
 template <int K, bool RESIDENT>
 __global__ __launch_bounds__(kIstaThreads, 2) void k_ista(IstaParams p) {
     constexpr int NQ = K / 16;
-    __shared__ IstaSmem<K> S;
+    __shared__ __attribute__((aligned(16))) IstaSmem<K> S;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int jl = lane & 15, g = lane >> 4;

@@ -2,13 +2,17 @@
 // SVT(X + (1/mu_2)*lambda_2, 1/mu_2)).
 //
 // The reference runs a float32 LAPACK SVD of the P x B matrix.  Here, MI355X-first:
-//   1. fp64 Gram Z^T Z over row slabs (many workgroups, coalesced rows) + a fixed-order reduce;
-//   2. one workgroup runs a cyclic parallel (round-robin) two-sided Jacobi eigensolver on the
-//      B x B Gram in fp64, WARM-STARTED from the previous outer iteration's eigenvectors
-//      (A0 = V^T G V is nearly diagonal, so 1-3 sweeps instead of ~8);
-//   3. E = V diag(min(tau/s, 1)) V^T and U = Z - Z E (f32 accumulate; E is small, so its
-//      float32 rounding costs << 1e-6 relative).  Z V diag((s-tau)_+/s) V^T == U_s (S-tau)_+ V_h.
-// The Gram/eig stage runs on its own stream beside the sparse-coding kernel.
+//   1. fp64 Gram G = Z^T Z over row slabs (many workgroups, coalesced rows), fixed-order reduce;
+//   2. warm start: A0 = V^T G V with the previous outer iteration's eigenvectors (tiled fp64
+//      GEMMs) — nearly diagonal, so Jacobi needs 1-3 sweeps instead of ~8;
+//   3. ONE workgroup runs a cyclic parallel (round-robin) two-sided Jacobi on A held in LDS as a
+//      packed fp64 upper triangle (B <= 200: <= 160,800 B), logging each round's rotations;
+//   4. the eigenvector update V <- V J_1 ... J_R is replayed from the log row by row in parallel
+//      (rows of V evolve independently), off the Jacobi workgroup's critical path;
+//   5. E = V diag(min(tau/s, 1)) V^T (fp64 -> f32) and U = Z - Z E.
+//      Z V diag((s-tau)_+/s) V^T == U_s (S-tau)_+ V_h, and E is small so its f32 rounding costs
+//      << 1e-6 relative in U.
+// The whole chain runs on its own stream beside the sparse-coding kernel.
 #include <math.h>
 
 #include "lrs_common.h"
@@ -19,15 +23,19 @@ constexpr int kGramTile = 32;
 constexpr int kGramRows = 1024;   // rows per slab
 constexpr int kGramChunk = 64;    // rows staged per LDS chunk
 constexpr int kJacobiThreads = 1024;
+constexpr int kMaxBp = 200;       // packed fp64 triangle of 200 x 200 = 160,800 B of LDS
+constexpr int kMaxSweeps = 40;
 
 struct SvtWs {
     double *partial;  // [nslab][ntile_pairs][32*32]
     double *G;        // [Bp][Bp]
-    double *A;        // [Bp][Bp]
-    double *V;        // [Bp][Bp]
-    double *T;        // [Bp][Bp] scratch
+    double *A0;       // [Bp][Bp]  V^T G V (warm start)
+    double *T;        // [Bp][Bp]  scratch
+    double *V[2];     // [Bp][Bp]  eigenvectors, double-buffered
+    double *lam;      // [Bp]      eigenvalues (diag of the converged A)
+    double *rot;      // [kMaxSweeps*(Bp-1)][Bp/2][2]  (c, s) per round and pair
     float *E;         // [B][B]
-    int *state;       // [0] = V valid (warm start available), [1] = sweeps used last call
+    int *state;       // [0] V valid, [1] current V buffer, [2] rounds, [3] sweeps
     int64_t nslab, ntp, Bp;
 };
 
@@ -45,12 +53,16 @@ static SvtWs svt_ws_layout(void *base, int64_t P, int64_t B) {
         p += (bytes + 255) / 256 * 256;
         return r;
     };
+    const size_t mat = (size_t)w.Bp * w.Bp * sizeof(double);
     w.state = (int *)take(256);
     w.partial = (double *)take((size_t)w.nslab * w.ntp * kGramTile * kGramTile * sizeof(double));
-    w.G = (double *)take((size_t)w.Bp * w.Bp * sizeof(double));
-    w.A = (double *)take((size_t)w.Bp * w.Bp * sizeof(double));
-    w.V = (double *)take((size_t)w.Bp * w.Bp * sizeof(double));
-    w.T = (double *)take((size_t)w.Bp * w.Bp * sizeof(double));
+    w.G = (double *)take(mat);
+    w.A0 = (double *)take(mat);
+    w.T = (double *)take(mat);
+    w.V[0] = (double *)take(mat);
+    w.V[1] = (double *)take(mat);
+    w.lam = (double *)take((size_t)w.Bp * sizeof(double));
+    w.rot = (double *)take((size_t)kMaxSweeps * (w.Bp - 1) * (w.Bp / 2) * 2 * sizeof(double));
     w.E = (float *)take((size_t)B * B * sizeof(float));
     return w;
 }
@@ -58,6 +70,13 @@ static SvtWs svt_ws_layout(void *base, int64_t P, int64_t B) {
 static size_t svt_ws_bytes(int64_t P, int64_t B) {
     SvtWs w = svt_ws_layout(nullptr, P, B);
     return (size_t)((char *)(w.E + B * B) - (char *)nullptr) + 256;
+}
+
+// Round-robin (circle method) pair k of round r over indices 0..Bp-1, returned with p < q.
+__device__ __forceinline__ void rr_pair(int r, int k, int Bp, int &p, int &q) {
+    if (k == 0) { p = Bp - 1; q = r; }
+    else { p = (r + k) % (Bp - 1); q = (r - k + (Bp - 1)) % (Bp - 1); }
+    if (p > q) { int t = p; p = q; q = t; }
 }
 
 // ---- 1. partial Gram over a slab of rows, one 32x32 upper-triangular tile pair per workgroup --
@@ -124,156 +143,252 @@ __global__ __launch_bounds__(256) void k_gram_reduce(const double *__restrict__ 
         const int i = ti * kGramTile + e / kGramTile, j = tj * kGramTile + e % kGramTile;
         double s = 0.0;
         for (int64_t sl = 0; sl < nslab; ++sl) s += partial[(sl * ntp + tp) * (kGramTile * kGramTile) + e];
-        if (i < B && j < B) {
-            G[(int64_t)i * Bp + j] = s;
-            G[(int64_t)j * Bp + i] = s;
+        if (i < Bp && j < Bp) {
+            const double v = (i < B && j < B) ? s : 0.0;   // pad row/col (B odd) is zero
+            G[(int64_t)i * Bp + j] = v;
+            G[(int64_t)j * Bp + i] = v;
         }
     }
 }
 
-// ---- 2. one-workgroup cyclic parallel Jacobi + E = V diag(min(tau/s,1)) V^T ------------------
-__device__ __forceinline__ double block_sum(double v, double *red) {
+// ---- 2. warm start A0 = V^T (G V) with the current V (16 x 16 fp64 tiles) -------------------
+// stage 0: T = G V ; stage 1: A0 = V^T T.  The current V buffer index lives on the device.
+__global__ __launch_bounds__(256) void k_gemm_f64_state(SvtWs w, int stage) {
+    __shared__ double As[16][17], Bs[16][17];
+    const int n = (int)w.Bp;
+    const double *V = w.V[w.state[1]];
+    const double *A = stage == 0 ? w.G : V;
+    const double *Bm = stage == 0 ? V : w.T;
+    double *C = stage == 0 ? w.T : w.A0;
+    const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+    const int i = blockIdx.y * 16 + ty, j = blockIdx.x * 16 + tx;
+    double acc = 0.0;
+    for (int k0 = 0; k0 < n; k0 += 16) {
+        const int ka = k0 + tx, kb = k0 + ty;
+        if (stage == 1) As[ty][tx] = (i < n && ka < n) ? A[(int64_t)ka * n + i] : 0.0;   // (V^T)[i][ka]
+        else As[ty][tx] = (i < n && ka < n) ? A[(int64_t)i * n + ka] : 0.0;
+        Bs[ty][tx] = (kb < n && j < n) ? Bm[(int64_t)kb * n + j] : 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = __fma_rn(As[ty][k], Bs[k][tx], acc);
+        __syncthreads();
+    }
+    if (i < n && j < n) C[(int64_t)i * n + j] = acc;
+}
+
+// ---- 3. one-workgroup Jacobi on the packed upper triangle in LDS -----------------------------
+// Table-driven: per round the pair indices (ip, iq) and rotations (rc, rs) go to LDS once, the
+// packed index of (i <= j) is rowoff[i] + j, and the 2x2 block updates are mapped on a 32 x 32
+// thread grid (shifts, no divisions in the inner loop).
+__device__ __forceinline__ double wg_reduce(double v, double *red) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    const int w = threadIdx.x >> 6;
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     double s = 0.0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+#pragma unroll
+    for (int i = 0; i < kJacobiThreads / 64; ++i) s += red[i];
     return s;
 }
 
-__global__ __launch_bounds__(kJacobiThreads) void k_jacobi_svt(SvtWs w, int B, double tau, int warm, int max_sweeps,
-                                                               double *__restrict__ s_out) {
-    const int Bp = (int)w.Bp;  // even
-    const int half = Bp / 2;
+__global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm) {
+    extern __shared__ double sm[];
+    const int Bp = (int)w.Bp, half = Bp / 2;
+    const int npk = Bp * (Bp + 1) / 2;
+    double *A = sm;                      // packed upper triangle
+    double *rc = A + npk, *rs = rc + half, *red = rs + half;
+    int *ip = (int *)(red + 16), *iq = ip + half, *rowoff = iq + half;
     const int tid = threadIdx.x;
-    __shared__ double red[kJacobiThreads / 64];
-    __shared__ double rc[512], rs[512];
-    __shared__ int rp[512], rq[512];
-    __shared__ double lam[512];
-    __shared__ int order[512];
-    const int64_t BB = (int64_t)Bp * Bp;
     const bool use_warm = warm && w.state[0] == 1;
-    // A0 = V^T G V (warm) or G (cold).  Padding row/col (B odd) is an isolated zero eigenpair.
-    if (use_warm) {
-        for (int64_t idx = tid; idx < BB; idx += kJacobiThreads) {    // T = G V
-            const int i = (int)(idx / Bp), j = (int)(idx % Bp);
-            double s = 0.0;
-            for (int k = 0; k < Bp; ++k) s = __fma_rn(w.G[(int64_t)i * Bp + k], w.V[(int64_t)k * Bp + j], s);
-            w.T[idx] = s;
-        }
-        __syncthreads();
-        for (int64_t idx = tid; idx < BB; idx += kJacobiThreads) {    // A = V^T T
-            const int i = (int)(idx / Bp), j = (int)(idx % Bp);
-            double s = 0.0;
-            for (int k = 0; k < Bp; ++k) s = __fma_rn(w.V[(int64_t)k * Bp + i], w.T[(int64_t)k * Bp + j], s);
-            w.A[idx] = s;
-        }
-    } else {
-        for (int64_t idx = tid; idx < BB; idx += kJacobiThreads) {
-            const int i = (int)(idx / Bp), j = (int)(idx % Bp);
-            w.A[idx] = (i < B && j < B) ? w.G[idx] : 0.0;
-            w.V[idx] = (i == j) ? 1.0 : 0.0;
-        }
-    }
+    const double *src = use_warm ? w.A0 : w.G;
+    for (int i = tid; i < Bp; i += kJacobiThreads) rowoff[i] = i * Bp - (i * (i - 1)) / 2 - i;
     __syncthreads();
-    double diag2 = 0.0;
-    for (int i = tid; i < Bp; i += kJacobiThreads) diag2 += w.A[(int64_t)i * Bp + i] * w.A[(int64_t)i * Bp + i];
-    double off2 = 0.0;
-    for (int64_t idx = tid; idx < BB; idx += kJacobiThreads) {
-        const int i = (int)(idx / Bp), j = (int)(idx % Bp);
-        if (i != j) off2 += w.A[idx] * w.A[idx];
-    }
-    double dn = block_sum(diag2, red);
-    double of = block_sum(off2, red);
-    int sweeps = 0;
-    const double tol2 = 1e-30;  // (1e-15)^2 relative
-    while (sweeps < max_sweeps && of > tol2 * (dn + of)) {
+    for (int i = 0; i < Bp; ++i)
+        for (int j = i + tid; j < Bp; j += kJacobiThreads) A[rowoff[i] + j] = src[(int64_t)i * Bp + j];
+    __syncthreads();
+    auto norms = [&](double &dn, double &of) {
+        double d2 = 0.0, o2 = 0.0;
+        for (int i = 0; i < Bp; ++i)
+            for (int j = i + tid; j < Bp; j += kJacobiThreads) {
+                const double v = A[rowoff[i] + j];
+                if (i == j) d2 += v * v; else o2 += 2.0 * v * v;
+            }
+        dn = wg_reduce(d2, red);
+        of = wg_reduce(o2, red);
+    };
+    double dn, of;
+    norms(dn, of);
+    int sweeps = 0, rounds = 0;
+    const double tol2 = 1e-26;   // off(A) <= 1e-13 ||A||
+    const int a0 = tid >> 5, b0 = tid & 31;
+    while (sweeps < kMaxSweeps && of > tol2 * (dn + of)) {
         for (int r = 0; r < Bp - 1; ++r) {
-            // round-robin pairing (circle method) over indices 0..Bp-1
-            for (int k = tid; k < half; k += kJacobiThreads) {
+            if (tid < half) {
                 int p, q;
-                if (k == 0) { p = Bp - 1; q = r; }
-                else { p = (r + k) % (Bp - 1); q = (r - k + (Bp - 1)) % (Bp - 1); }
-                if (p > q) { int t = p; p = q; q = t; }
-                const double app = w.A[(int64_t)p * Bp + p], aqq = w.A[(int64_t)q * Bp + q];
-                const double apq = w.A[(int64_t)p * Bp + q];
+                rr_pair(r, tid, Bp, p, q);
+                const double app = A[rowoff[p] + p], aqq = A[rowoff[q] + q], apq = A[rowoff[p] + q];
                 double c = 1.0, s = 0.0;
-                if (apq != 0.0 && fabs(apq) > 1e-300) {
+                if (apq != 0.0) {
                     const double theta = (aqq - app) / (2.0 * apq);
                     const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                     c = 1.0 / sqrt(t * t + 1.0);
                     s = t * c;
                 }
-                rp[k] = p; rq[k] = q; rc[k] = c; rs[k] = s;
+                ip[tid] = p;
+                iq[tid] = q;
+                rc[tid] = c;
+                rs[tid] = s;
+                double *log = w.rot + ((int64_t)rounds * half + tid) * 2;
+                log[0] = c;
+                log[1] = s;
             }
             __syncthreads();
-            // A <- J^T A J on every 2x2 block (k1,k2); J = [[c, s], [-s, c]] on (p, q)
-            for (int idx = tid; idx < half * half; idx += kJacobiThreads) {
-                const int k1 = idx / half, k2 = idx % half;
-                const int p1 = rp[k1], q1 = rq[k1], p2 = rp[k2], q2 = rq[k2];
-                const double c1 = rc[k1], s1 = rs[k1], c2 = rc[k2], s2 = rs[k2];
-                double *App = &w.A[(int64_t)p1 * Bp + p2], *Apq = &w.A[(int64_t)p1 * Bp + q2];
-                double *Aqp = &w.A[(int64_t)q1 * Bp + p2], *Aqq = &w.A[(int64_t)q1 * Bp + q2];
-                const double a = *App, b = *Apq, cc = *Aqp, d = *Aqq;
-                // left: rows (p1,q1) by J1^T ; right: cols (p2,q2) by J2
-                const double la = c1 * a - s1 * cc, lb = c1 * b - s1 * d;
-                const double lc = s1 * a + c1 * cc, ld = s1 * b + c1 * d;
-                double na = c2 * la - s2 * lb, nb = s2 * la + c2 * lb;
-                double nc = c2 * lc - s2 * ld, nd = s2 * lc + c2 * ld;
-                if (k1 == k2) { nb = 0.0; nc = 0.0; }
-                *App = na; *Apq = nb; *Aqp = nc; *Aqq = nd;
-            }
-            for (int idx = tid; idx < Bp * half; idx += kJacobiThreads) {   // V <- V J
-                const int i = idx / half, k = idx % half;
-                double *vp = &w.V[(int64_t)i * Bp + rp[k]], *vq = &w.V[(int64_t)i * Bp + rq[k]];
-                const double a = *vp, b = *vq;
-                *vp = rc[k] * a - rs[k] * b;
-                *vq = rs[k] * a + rc[k] * b;
+            // A <- J^T A J on every unordered 2x2 block (k1 <= k2); J = [[c, s], [-s, c]] on (p, q)
+            for (int k1 = a0; k1 < half; k1 += 32) {
+                const int p1 = ip[k1], q1 = iq[k1];
+                const double c1 = rc[k1], s1 = rs[k1];
+                const int ro_p1 = rowoff[p1], ro_q1 = rowoff[q1];
+                for (int k2 = b0; k2 < half; k2 += 32) {
+                    if (k2 < k1) continue;
+                    const double c2 = rc[k2], s2 = rs[k2];
+                    if (k1 == k2) {
+                        const int ipp = ro_p1 + p1, iqq = ro_q1 + q1, ipq = ro_p1 + q1;
+                        const double a = A[ipp], b = A[ipq], d = A[iqq];
+                        const double la = c1 * a - s1 * b, lb = c1 * b - s1 * d;
+                        const double lc = s1 * a + c1 * b, ld = s1 * b + c1 * d;
+                        A[ipp] = c1 * la - s1 * lb;
+                        A[iqq] = s1 * lc + c1 * ld;
+                        A[ipq] = 0.0;
+                    } else {
+                        const int p2 = ip[k2], q2 = iq[k2];
+                        const int i00 = p1 <= p2 ? ro_p1 + p2 : rowoff[p2] + p1;
+                        const int i01 = p1 <= q2 ? ro_p1 + q2 : rowoff[q2] + p1;
+                        const int i10 = q1 <= p2 ? ro_q1 + p2 : rowoff[p2] + q1;
+                        const int i11 = q1 <= q2 ? ro_q1 + q2 : rowoff[q2] + q1;
+                        const double a = A[i00], b = A[i01], cc = A[i10], d = A[i11];
+                        const double la = c1 * a - s1 * cc, lb = c1 * b - s1 * d;
+                        const double lc = s1 * a + c1 * cc, ld = s1 * b + c1 * d;
+                        A[i00] = c2 * la - s2 * lb;
+                        A[i01] = s2 * la + c2 * lb;
+                        A[i10] = c2 * lc - s2 * ld;
+                        A[i11] = s2 * lc + c2 * ld;
+                    }
+                }
             }
             __syncthreads();
+            ++rounds;
         }
         ++sweeps;
-        diag2 = 0.0; off2 = 0.0;
-        for (int i = tid; i < Bp; i += kJacobiThreads) diag2 += w.A[(int64_t)i * Bp + i] * w.A[(int64_t)i * Bp + i];
-        for (int64_t idx = tid; idx < BB; idx += kJacobiThreads) {
-            const int i = (int)(idx / Bp), j = (int)(idx % Bp);
-            if (i != j) off2 += w.A[idx] * w.A[idx];
-        }
-        dn = block_sum(diag2, red);
-        of = block_sum(off2, red);
+        norms(dn, of);
     }
-    // eigenvalues -> singular values -> shrink factors e_k = min(tau/s_k, 1) (1 - phi)
-    for (int i = tid; i < Bp; i += kJacobiThreads) {
-        const double l = w.A[(int64_t)i * Bp + i];
-        lam[i] = l > 0.0 ? sqrt(l) : 0.0;
+    for (int i = tid; i < Bp; i += kJacobiThreads) w.lam[i] = A[rowoff[i] + i];
+    if (tid == 0) {
+        w.state[2] = rounds;
+        w.state[3] = sweeps;
     }
-    __syncthreads();
-    if (s_out && tid == 0) {
-        // selection order by descending s (B <= 512, serial is fine, once per call)
-        for (int i = 0; i < Bp; ++i) order[i] = i;
-        for (int i = 0; i < Bp; ++i)
-            for (int k = i + 1; k < Bp; ++k)
-                if (lam[order[k]] > lam[order[i]]) { int t = order[i]; order[i] = order[k]; order[k] = t; }
-        for (int i = 0; i < B; ++i) s_out[i] = lam[order[i]];
-    }
-    __syncthreads();
-    for (int i = tid; i < Bp; i += kJacobiThreads) {
-        const double s = lam[i];
-        lam[i] = (s > tau) ? tau / s : 1.0;
-    }
-    __syncthreads();
-    for (int64_t idx = tid; idx < (int64_t)B * B; idx += kJacobiThreads) {
-        const int i = (int)(idx / B), j = (int)(idx % B);
-        double s = 0.0;
-        for (int k = 0; k < Bp; ++k) s = __fma_rn(w.V[(int64_t)i * Bp + k] * lam[k], w.V[(int64_t)j * Bp + k], s);
-        w.E[idx] = (float)s;
-    }
-    if (tid == 0) { w.state[0] = 1; w.state[1] = sweeps; }
 }
 
-// ---- 3. U = Z - Z E  (64 x 64 output tile per workgroup, f32) ------------------------------
+// ---- 4. V_new = V_old J_1 ... J_R, 64 rows per 1024-thread workgroup, rows in LDS ------------
+constexpr int kVRows = 64;
+
+__global__ __launch_bounds__(1024) void k_jacobi_vrebuild(SvtWs w, int warm) {
+    extern __shared__ double vrow[];               // [kVRows][Bp]
+    __shared__ double lc[kMaxBp / 2], ls[kMaxBp / 2];
+    __shared__ int lp[kMaxBp / 2], lq[kMaxBp / 2];
+    const int Bp = (int)w.Bp, half = Bp / 2;
+    const int i0 = blockIdx.x * kVRows;
+    const int nrows = min(kVRows, Bp - i0);
+    const bool use_warm = warm && w.state[0] == 1;
+    const int cur = w.state[1];
+    const double *Vo = w.V[cur];
+    double *Vn = w.V[cur ^ 1];
+    for (int idx = threadIdx.x; idx < nrows * Bp; idx += 1024) {
+        const int rr = idx / Bp, j = idx % Bp, i = i0 + rr;
+        vrow[rr * Bp + j] = use_warm ? Vo[(int64_t)i * Bp + j] : (i == j ? 1.0 : 0.0);
+    }
+    const int rounds = w.state[2];
+    const int rr = threadIdx.x >> 4, kk = threadIdx.x & 15;
+    for (int rd = 0; rd < rounds; ++rd) {
+        __syncthreads();
+        if (threadIdx.x < half) {
+            int p, q;
+            rr_pair(rd % (Bp - 1), threadIdx.x, Bp, p, q);
+            const double *log = w.rot + ((int64_t)rd * half + threadIdx.x) * 2;
+            lp[threadIdx.x] = p;
+            lq[threadIdx.x] = q;
+            lc[threadIdx.x] = log[0];
+            ls[threadIdx.x] = log[1];
+        }
+        __syncthreads();
+        if (rr < nrows) {
+            double *row = vrow + rr * Bp;
+            for (int k = kk; k < half; k += 16) {
+                const int p = lp[k], q = lq[k];
+                const double c = lc[k], s = ls[k];
+                const double vp = row[p], vq = row[q];
+                row[p] = c * vp - s * vq;
+                row[q] = s * vp + c * vq;
+            }
+        }
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nrows * Bp; idx += 1024) {
+        const int r2 = idx / Bp, j = idx % Bp;
+        Vn[(int64_t)(i0 + r2) * Bp + j] = vrow[r2 * Bp + j];
+    }
+}
+
+__global__ void k_svt_finish_state(SvtWs w) {
+    // flip the current-V buffer; V is now valid for warm starts
+    w.state[1] ^= 1;
+    w.state[0] = 1;
+}
+
+// ---- 5a. E = V diag(e) V^T, e_k = min(tau/s_k, 1); s_out = sorted singular values -----------
+__global__ __launch_bounds__(256) void k_build_E(SvtWs w, int B, double tau) {
+    __shared__ double Vi[16][17], Vj[16][17], ek[16];
+    const int Bp = (int)w.Bp;
+    const double *V = w.V[w.state[1]];
+    const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+    const int i = blockIdx.y * 16 + ty, jrow0 = blockIdx.x * 16;
+    const int j = jrow0 + tx;
+    double acc = 0.0;
+    for (int k0 = 0; k0 < Bp; k0 += 16) {
+        Vi[ty][tx] = (i < Bp && k0 + tx < Bp) ? V[(int64_t)i * Bp + k0 + tx] : 0.0;
+        Vj[ty][tx] = (jrow0 + ty < Bp && k0 + tx < Bp) ? V[(int64_t)(jrow0 + ty) * Bp + k0 + tx] : 0.0;
+        if (threadIdx.x < 16) {
+            const int k = k0 + threadIdx.x;
+            double e = 0.0;
+            if (k < Bp) {
+                const double l = w.lam[k];
+                const double s = l > 0.0 ? sqrt(l) : 0.0;
+                e = (s > tau) ? tau / s : 1.0;
+            }
+            ek[threadIdx.x] = e;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = __fma_rn(Vi[ty][k] * ek[k], Vj[tx][k], acc);
+        __syncthreads();
+    }
+    if (i < B && j < B) w.E[(int64_t)i * B + j] = (float)acc;
+}
+
+__global__ __launch_bounds__(256) void k_sorted_singular_values(SvtWs w, int B, double *__restrict__ s_out) {
+    // rank of each eigenvalue (ties broken by index) -> descending order
+    const int Bp = (int)w.Bp;
+    for (int i = threadIdx.x; i < Bp; i += blockDim.x) {
+        const double li = w.lam[i];
+        int rank = 0;
+        for (int k = 0; k < Bp; ++k) {
+            const double lk = w.lam[k];
+            rank += (lk > li) || (lk == li && k < i);
+        }
+        if (rank < B) s_out[rank] = li > 0.0 ? sqrt(li) : 0.0;
+    }
+}
+
+// ---- 5b. U = Z - Z E  (64 x 64 output tile per workgroup, f32) ------------------------------
 constexpr int kAT = 64;   // output tile
 constexpr int kAK = 16;   // k chunk
 
@@ -290,7 +405,7 @@ __global__ __launch_bounds__(256) void k_svt_apply(const float *__restrict__ X, 
     for (int k0 = 0; k0 < B; k0 += kAK) {
         __syncthreads();
         for (int idx = tid; idx < kAK * kAT; idx += 256) {
-            const int rr = idx / kAK, kk = idx % kAK;      // Z: row-major, k fastest -> coalesced-ish
+            const int rr = idx / kAK, kk = idx % kAK;
             const int64_t r = r0 + rr;
             const int k = k0 + kk;
             float z = 0.f;
@@ -344,24 +459,54 @@ extern "C" size_t lrs_svt_workspace(int64_t P, int64_t B) {
 extern "C" int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau, float *U,
                            double *s_out, int warm, void *ws, size_t ws_bytes, void *stream) {
     if (!X || !U || !ws || P <= 0 || B <= 0 || tau < 0.0) return LRS_E_INVALID;
-    if (B > 510) return LRS_E_UNSUPPORTED;
+    if (B + (B & 1) > kMaxBp) return LRS_E_UNSUPPORTED;
     if (ws_bytes < svt_ws_bytes(P, B)) return LRS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
     SvtWs w = svt_ws_layout(ws, P, B);
     if (!warm) {
-        hipError_t e = hipMemsetAsync(w.state, 0, sizeof(int) * 2, st);
+        hipError_t e = hipMemsetAsync(w.state, 0, sizeof(int) * 4, st);
         if (e != hipSuccess) return (int)e;
     }
     const int nt = (int)gram_ntiles(B);
+    const int Bp = (int)w.Bp;
     hipLaunchKernelGGL(k_gram_partial, dim3((unsigned)w.ntp, (unsigned)w.nslab), dim3(256), 0, st, X, L2, c2, P,
                        (int)B, nt, w.partial);
     LRS_CHECK_LAUNCH();
     const int64_t tot = w.ntp * kGramTile * kGramTile;
     hipLaunchKernelGGL(k_gram_reduce, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 4096)), dim3(256), 0, st,
-                       w.partial, w.nslab, (int)w.ntp, nt, (int)B, (int)w.Bp, w.G);
+                       w.partial, w.nslab, (int)w.ntp, nt, (int)B, Bp, w.G);
     LRS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_jacobi_svt, dim3(1), dim3(kJacobiThreads), 0, st, w, (int)B, tau, warm, 30, s_out);
+    if (warm) {
+        // A0 = V^T (G V) with the current V (no-op result if V is not valid yet: the Jacobi
+        // kernel then starts from G)
+        const dim3 g16((Bp + 15) / 16, (Bp + 15) / 16);
+        hipLaunchKernelGGL(k_gemm_f64_state, g16, dim3(256), 0, st, w, 0);
+        LRS_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_gemm_f64_state, g16, dim3(256), 0, st, w, 1);
+        LRS_CHECK_LAUNCH();
+    }
+    const size_t smem = sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp + 16) + sizeof(int) * (2 * Bp);
+    const size_t vsmem = sizeof(double) * (size_t)kVRows * Bp;
+    // dynamic LDS above 64 KiB must be opted into; request exactly what this shape needs
+    hipError_t ea = hipFuncSetAttribute((const void *)k_jacobi_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)smem);
+    if (ea != hipSuccess) return (int)ea;
+    ea = hipFuncSetAttribute((const void *)k_jacobi_vrebuild, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vsmem);
+    if (ea != hipSuccess) return (int)ea;
+    hipLaunchKernelGGL(k_jacobi_lds, dim3(1), dim3(kJacobiThreads), smem, st, w, warm);
     LRS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_jacobi_vrebuild, dim3((unsigned)((Bp + kVRows - 1) / kVRows)), dim3(1024), vsmem, st, w,
+                       warm);
+    LRS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_svt_finish_state, dim3(1), dim3(1), 0, st, w);
+    LRS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_build_E, dim3((unsigned)((B + 15) / 16), (unsigned)((B + 15) / 16)), dim3(256), 0, st, w,
+                       (int)B, tau);
+    LRS_CHECK_LAUNCH();
+    if (s_out) {
+        hipLaunchKernelGGL(k_sorted_singular_values, dim3(1), dim3(256), 0, st, w, (int)B, s_out);
+        LRS_CHECK_LAUNCH();
+    }
     dim3 grid((unsigned)((P + kAT - 1) / kAT), (unsigned)((B + kAT - 1) / kAT));
     hipLaunchKernelGGL(k_svt_apply, grid, dim3(256), 0, st, X, L2, c2, w.E, P, (int)B, U);
     LRS_CHECK_LAUNCH();

@@ -127,8 +127,8 @@ class LrsPnP:
         main = torch.cuda.current_stream()
         lr = self.lowrank_stream
         lr.wait_stream(main)
-        self.sparse_coding(stream=main)
-        self.low_rank(stream=lr)
+        self.low_rank(stream=lr)          # queued first: its Gram kernels grab the chip briefly,
+        self.sparse_coding(stream=main)   # then the one-workgroup eigensolver runs beside ISTA
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
                         self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# GPU box helper: tests, smoke, bench, kernel-trace profile.  Each GPU step has its own limit.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+tag=${1:-r01}
+timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/smoke.log; exit 1; }
+timeout -k 10 400 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench failed; tail gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || { echo prof failed; tail gpurun_out/bench_prof.err; exit 1; }
+echo all-ok
