@@ -101,6 +101,13 @@ int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n,
 size_t lrs_svt_workspace(int64_t P, int64_t B);
 int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau,
                 float *U, double *s_out, int warm, void *ws, size_t ws_bytes, void *stream);
+/* The same call split in two stream-ordered halves so the caller can start the sparse-coding
+ * kernel between them: _gram (multi-workgroup Gram + warm-start products, ~0.3 ms) and _finish
+ * (one-workgroup eigensolver + V update + U, which then runs beside the sparse coding). */
+int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, int warm,
+                     void *ws, size_t ws_bytes, void *stream);
+int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau,
+                       float *U, double *s_out, int warm, void *ws, size_t ws_bytes, void *stream);
 
 /* ---- col2im + closed-form X update + dual updates ------------------------------------------
  * IMout = sum over covering blocks (block order) of phi, Weight = count, lambda1_sum = repeated

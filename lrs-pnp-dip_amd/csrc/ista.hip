@@ -33,6 +33,15 @@ struct alignas(16) IstaSmem {
     float DT[K][kStageRows + 4];  // [atom][row]
 };
 
+// a / b from the correctly rounded reciprocal y = 1/b with one Markstein correction step:
+// q = a*y, r = fma(-b, q, a) (exact), q + r*y.  Equals the IEEE quotient a/b (the reference's
+// torch division) away from overflow/underflow, at 3 instructions instead of ~10.
+__device__ __forceinline__ float div_by(float a, float b, float y) {
+    const float q = a * y;
+    const float r = __fmaf_rn(-b, q, a);
+    return __fmaf_rn(r, y, q);
+}
+
 struct IstaParams {
     const float *Yb;
     const uint8_t *obs;
@@ -92,32 +101,48 @@ __device__ __forceinline__ void dict_t_times_r(const IstaSmem<K> &S, int t, cons
 }
 
 // The 4 NLM outputs of one chunk; w[0..10] = v-hat[a0-3 .. a0+7] (a0 = first atom of chunk).
-__device__ __forceinline__ void nlm_chunk(const double (&w)[11], double inv2, double c0, float (&out)[4]) {
-    double s1[10], s2[9], s3[8];
+// Each symmetric weight w(i,+t) == w(i+t,-t) is computed once: 18 weights for 4 outputs.
+__device__ __forceinline__ void nlm_chunk(const double (&w)[11], double kneg, double c0, float (&out)[4]) {
+    int W1[7], W2[7], W3[7];      // W_t[i] = hi word of w(a0-3+i, +t), s_t[i] = (w[i] - w[i+t])^2
+    {
+        double sp = (w[2] - w[3]) * (w[2] - w[3]);
 #pragma unroll
-    for (int i = 0; i < 10; ++i) { double d = w[i] - w[i + 1]; s1[i] = d * d; }
+        for (int i = 2; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 2], sn = d * d;
+            W1[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
+    {
+        double sp = (w[1] - w[3]) * (w[1] - w[3]);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) { double d = w[i] - w[i + 2]; s2[i] = d * d; }
+        for (int i = 1; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 3], sn = d * d;
+            W2[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
+    {
+        double sp = (w[0] - w[3]) * (w[0] - w[3]);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { double d = w[i] - w[i + 3]; s3[i] = d * d; }
+        for (int i = 0; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 4], sn = d * d;
+            W3[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int C = 3 + e;
         // t = -3,-2,-1,+1,+2,+3 (the canonical order of oracle_nlm_col)
-        const double Dm3 = (s3[C - 3] + s3[C - 2]) * inv2;
-        const double Dm2 = (s2[C - 2] + s2[C - 1]) * inv2;
-        const double Dm1 = (s1[C - 1] + s1[C]) * inv2;
-        const double Dp1 = (s1[C] + s1[C + 1]) * inv2;
-        const double Dp2 = (s2[C] + s2[C + 1]) * inv2;
-        const double Dp3 = (s3[C] + s3[C + 1]) * inv2;
-        const double Ds[6] = {Dm3, Dm2, Dm1, Dp1, Dp2, Dp3};
-        const double Vs[6] = {w[C - 3], w[C - 2], w[C - 1], w[C + 1], w[C + 2], w[C + 3]};
+        const double ws[6] = {hi_to_double(W3[C - 3]), hi_to_double(W2[C - 2]), hi_to_double(W1[C - 1]),
+                              hi_to_double(W1[C]), hi_to_double(W2[C]), hi_to_double(W3[C])};
+        const double vs[6] = {w[C - 3], w[C - 2], w[C - 1], w[C + 1], w[C + 2], w[C + 3]};
         double sw = 0.0, swv = 0.0;
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-            const double wt = (Ds[k] > kNlmCutoff) ? 0.0 : nlm_fast_exp(-Ds[k]);
-            sw = sw + wt;
-            swv = __fma_rn(wt, Vs[k], swv);
+            sw = sw + ws[k];
+            swv = __fma_rn(ws[k], vs[k], swv);
         }
         const double num = __fma_rn(7.0, swv, c0 * w[C]);
         const double den = __fma_rn(7.0, sw, c0);
@@ -125,52 +150,235 @@ __device__ __forceinline__ void nlm_chunk(const double (&w)[11], double inv2, do
     }
 }
 
+// Neighbour-exchange state for the in-register NLM along the atom axis.  A lane (block l&15,
+// group g = l>>4) holds atoms 16q+4g .. 16q+4g+3 of every 16-atom tile q; chunk c-1 lives in
+// lane l-16 (same tile, or tile q-1 when g == 0), chunk c+1 in lane l+16 (tile q+1 when g == 3).
+struct NlmLanes {
+    int g, src_prev, src_next;
+    __device__ __forceinline__ explicit NlmLanes(int lane)
+        : g(lane >> 4), src_prev((lane + 48) & 63), src_next((lane + 16) & 63) {}
+};
+
+// NLM of tile q given this lane's gradient chunk `own`, the shuffled neighbours of tiles q-1/q/q+1
+// (Pprev = prev-lane chunk of tile q-1, Pcur = of tile q; Ncur = next-lane chunk of tile q,
+// Nnext = of tile q+1), with numpy-style reflection at both ends of the K atoms.
+template <int NQ>
+__device__ __forceinline__ void nlm_tile(int q, const NlmLanes &L, const float (&own)[4], const float (&Pprev)[3],
+                                         const float (&Pcur)[3], const float (&Ncur)[4], const float (&Nnext)[4],
+                                         double kneg, double c0, float (&out)[4]) {
+    float prv[3], nxt[4];
+    if (L.g == 0) {
+        if (q == 0) { prv[0] = own[3]; prv[1] = own[2]; prv[2] = own[1]; }   // reflect
+        else { prv[0] = Pprev[0]; prv[1] = Pprev[1]; prv[2] = Pprev[2]; }
+    } else {
+        prv[0] = Pcur[0]; prv[1] = Pcur[1]; prv[2] = Pcur[2];
+    }
+    if (L.g == 3) {
+        if (q == NQ - 1) { nxt[0] = own[2]; nxt[1] = own[1]; nxt[2] = own[0]; nxt[3] = prv[2]; }
+        else { nxt[0] = Nnext[0]; nxt[1] = Nnext[1]; nxt[2] = Nnext[2]; nxt[3] = Nnext[3]; }
+    } else {
+        nxt[0] = Ncur[0]; nxt[1] = Ncur[1]; nxt[2] = Ncur[2]; nxt[3] = Ncur[3];
+    }
+    const double w[11] = {prv[0], prv[1], prv[2], own[0], own[1], own[2], own[3],
+                          nxt[0], nxt[1], nxt[2], nxt[3]};
+    nlm_chunk(w, kneg, c0, out);
+}
+
 // X <- NLM(G) along the atom axis, for this lane's block (4 atoms per 16-atom tile per lane).
 template <int K>
 __device__ __forceinline__ void nlm_prox_registers(const floatx4 (&G)[K / 16], float (&X)[K / 16][4],
                                                    double h, int lane) {
     constexpr int NQ = K / 16;
-    const int g = lane >> 4;
-    const int src_prev = (lane + 48) & 63;  // lane - 16: chunk c-1 (same q) or c-1 of q-1 (g == 0)
-    const int src_next = (lane + 16) & 63;  // lane + 16: chunk c+1 (same q) or c+1 of q+1 (g == 3)
-    const double inv2 = 2.0 / ((h * h) * 9.0);
+    const NlmLanes L(lane);
+    const double kneg = nlm_kneg(h);
     const double c0 = nlm_c0();
-    float Pprev[3], Pcur[3], Ncur[4], Nnext[4];
+    float Pprev[3] = {0.f, 0.f, 0.f}, Pcur[3], Ncur[4], Nnext[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) Ncur[e] = __shfl(G[0][e], src_next, 64);
-#pragma unroll
-    for (int e = 0; e < 3; ++e) { Pprev[e] = 0.f; Pcur[e] = 0.f; }
+    for (int e = 0; e < 4; ++e) Ncur[e] = __shfl(G[0][e], L.src_next, 64);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
 #pragma unroll
-        for (int e = 0; e < 3; ++e) Pcur[e] = __shfl(G[q][e + 1], src_prev, 64);
+        for (int e = 0; e < 3; ++e) Pcur[e] = __shfl(G[q][e + 1], L.src_prev, 64);
         if (q + 1 < NQ) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) Nnext[e] = __shfl(G[q + 1][e], src_next, 64);
+            for (int e = 0; e < 4; ++e) Nnext[e] = __shfl(G[q + 1][e], L.src_next, 64);
         }
-        float own[4] = {G[q][0], G[q][1], G[q][2], G[q][3]};
-        float prv[3], nxt[4];
-        if (g == 0) {
-            if (q == 0) { prv[0] = own[3]; prv[1] = own[2]; prv[2] = own[1]; }   // reflect
-            else { prv[0] = Pprev[0]; prv[1] = Pprev[1]; prv[2] = Pprev[2]; }
-        } else {
-            prv[0] = Pcur[0]; prv[1] = Pcur[1]; prv[2] = Pcur[2];
-        }
-        if (g == 3) {
-            if (q == NQ - 1) { nxt[0] = own[2]; nxt[1] = own[1]; nxt[2] = own[0]; nxt[3] = prv[2]; }
-            else { nxt[0] = Nnext[0]; nxt[1] = Nnext[1]; nxt[2] = Nnext[2]; nxt[3] = Nnext[3]; }
-        } else {
-            nxt[0] = Ncur[0]; nxt[1] = Ncur[1]; nxt[2] = Ncur[2]; nxt[3] = Ncur[3];
-        }
-        const double w[11] = {prv[0], prv[1], prv[2], own[0], own[1], own[2], own[3],
-                              nxt[0], nxt[1], nxt[2], nxt[3]};
+        const float own[4] = {G[q][0], G[q][1], G[q][2], G[q][3]};
         float o[4];
-        nlm_chunk(w, inv2, c0, o);
+        nlm_tile<NQ>(q, L, own, Pprev, Pcur, Ncur, Nnext, kneg, c0, o);
         X[q][0] = o[0]; X[q][1] = o[1]; X[q][2] = o[2]; X[q][3] = o[3];
 #pragma unroll
         for (int e = 0; e < 3; ++e) Pprev[e] = Pcur[e];
 #pragma unroll
         for (int e = 0; e < 4; ++e) Ncur[e] = Nnext[e];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Resident kernel (n_pad <= 64, i.e. bb <= 8): dictionary in LDS for the whole launch, y and the
+// row mask in VGPRs, and a software pipeline over the 16 atom tiles q of each inner iteration:
+//     MFMA : G[q+2] = D^T r (tile q+2)        | VALU : NLM of tile q -> x_new[q]
+//     MFMA : R_next += D[:, tile q] x_new[q]  | VALU : g[q+2] = x[q+2] + G[q+2]/alpha
+// so the matrix pipe works on the next products while the fp64 NLM of the current tile runs.
+// R_next = D x_new is complete when the last tile is done: it is the next iteration's residual
+// input and, after the last iteration, Phi = D x.
+// ------------------------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ floatx4 gemm2_tile(const IstaSmem<K> &S, int q, const float (&r)[4][4], int jl, int g) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 a = *reinterpret_cast<const float4 *>(&S.DT[16 * q + jl][16 * t + 4 * g]);
+        acc = mfma16x16x4(a.x, r[t][0], acc);
+        acc = mfma16x16x4(a.y, r[t][1], acc);
+        acc = mfma16x16x4(a.z, r[t][2], acc);
+        acc = mfma16x16x4(a.w, r[t][3], acc);
+    }
+    return acc;
+}
+
+template <int K>
+__device__ __forceinline__ void gemm1_tile(const IstaSmem<K> &S, int q, const float (&x)[4], floatx4 (&R)[4], int jl,
+                                           int g) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 a = *reinterpret_cast<const float4 *>(&S.DA[16 * t + jl][16 * q + 4 * g]);
+        R[t] = mfma16x16x4(a.x, x[0], R[t]);
+        R[t] = mfma16x16x4(a.y, x[1], R[t]);
+        R[t] = mfma16x16x4(a.z, x[2], R[t]);
+        R[t] = mfma16x16x4(a.w, x[3], R[t]);
+    }
+}
+
+// ABLATE (diagnostic builds only, never selected by lrs_ista_f32): 1 = prox replaced by a copy
+// (MFMA + data movement only), 2 = products replaced by register moves (NLM + movement only).
+template <int K, bool SOFT, int ABLATE = 0>
+__global__ __launch_bounds__(kIstaThreads, 2) void k_ista_res(IstaParams p) {
+    constexpr int NQ = K / 16;
+    __shared__ __attribute__((aligned(16))) IstaSmem<K> S;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int jl = lane & 15, g = lane >> 4;
+    const int64_t j = ((int64_t)blockIdx.x * kIstaWaves + wave) * 16 + jl;
+    const bool valid = j < p.nb;
+    const int NT = p.n_pad / 16;
+    const NlmLanes L(lane);
+
+    const float alpha = valid ? p.alpha[j] : 1.0f;
+    const double thr = valid ? p.thr[j] : 1.0;
+    const double kneg = nlm_kneg(thr);
+    const double c0 = nlm_c0();
+    const float Tsoft = (float)thr;
+
+    float y[4][4];
+    uint32_t mres = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        float4 yv = {0.f, 0.f, 0.f, 0.f};
+        uint32_t mv = 0;
+        if (valid && t < NT) {
+            yv = *reinterpret_cast<const float4 *>(&p.Yb[j * p.n_pad + 16 * t + 4 * g]);
+            mv = *reinterpret_cast<const uint32_t *>(&p.obs[j * p.n_pad + 16 * t + 4 * g]);
+        }
+        y[t][0] = yv.x; y[t][1] = yv.y; y[t][2] = yv.z; y[t][3] = yv.w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mres |= (((mv >> (8 * i)) & 0xffu) ? 1u : 0u) << (4 * t + i);
+    }
+    stage_dictionary<K>(S, p.D, p.n, 0);
+    __syncthreads();
+
+    float X[NQ][4];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) X[q][0] = X[q][1] = X[q][2] = X[q][3] = 0.f;
+    floatx4 R[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};   // D x for x = 0
+
+    const float ainv = 1.0f / alpha;
+    auto gradient = [&](floatx4 &Gq, const float (&xq)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Gq[i] = xq[i] + div_by(Gq[i], alpha, ainv);   // x + (D^T r)/alpha
+    };
+
+    for (int it = 0; it < p.Nit; ++it) {
+        float r[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[t][i] = ((mres >> (4 * t + i)) & 1u) ? (y[t][i] - R[t][i]) : 0.0f;
+            R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        floatx4 G[NQ];
+        auto gemm2 = [&](int q) -> floatx4 {
+            if (ABLATE == 2) {
+                floatx4 v = {r[q & 3][0], r[q & 3][1], r[q & 3][2], r[q & 3][3]};
+                return v;
+            }
+            return gemm2_tile<K>(S, q, r, jl, g);
+        };
+        G[0] = gemm2(0);
+        G[1] = gemm2(1);
+        __builtin_amdgcn_sched_barrier(0);
+        gradient(G[0], X[0]);
+        gradient(G[1], X[1]);
+        float Pprev[3] = {0.f, 0.f, 0.f}, Pcur[3], Ncur[4], Nnext[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Ncur[e] = __shfl(G[0][e], L.src_next, 64);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (q + 2 < NQ) G[q + 2] = gemm2(q + 2);
+            const float own[4] = {G[q][0], G[q][1], G[q][2], G[q][3]};
+            float o[4];
+            if (ABLATE == 1) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o[i] = own[i] * 0.5f;
+            } else if (SOFT) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float t = fabsf(own[i]) - Tsoft;
+                    t = t > 0.f ? t : 0.f;
+                    o[i] = own[i] > 0.f ? t : (own[i] < 0.f ? -t : 0.f);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 3; ++e) Pcur[e] = __shfl(G[q][e + 1], L.src_prev, 64);
+                if (q + 1 < NQ) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) Nnext[e] = __shfl(G[q + 1][e], L.src_next, 64);
+                }
+                nlm_tile<NQ>(q, L, own, Pprev, Pcur, Ncur, Nnext, kneg, c0, o);
+#pragma unroll
+                for (int e = 0; e < 3; ++e) Pprev[e] = Pcur[e];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Ncur[e] = Nnext[e];
+            }
+            X[q][0] = o[0]; X[q][1] = o[1]; X[q][2] = o[2]; X[q][3] = o[3];
+            if (ABLATE == 2) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) R[t] += floatx4{o[0], o[1], o[2], o[3]};
+            } else {
+                gemm1_tile<K>(S, q, X[q], R, jl, g);
+            }
+            if (q + 2 < NQ) gradient(G[q + 2], X[q + 2]);
+            // keep each pipeline step's LDS reads and MFMAs inside the step: without this fence
+            // the scheduler hoists every tile's ds_reads to the loop top and spills
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    if (valid) {
+        if (p.coefs) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                *reinterpret_cast<float4 *>(&p.coefs[j * K + 16 * q + 4 * g]) =
+                    make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
+        }
+        // Phi_z = Full_Dictionary @ Coefs == R (all rows, missing ones included)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t < NT)
+                *reinterpret_cast<float4 *>(&p.phi[j * p.n_pad + 16 * t + 4 * g]) =
+                    make_float4(R[t][0], R[t][1], R[t][2], R[t][3]);
     }
 }
 
@@ -255,7 +463,7 @@ __global__ __launch_bounds__(kIstaThreads, 2) void k_ista(IstaParams p) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) G[q][i] = X[q][i] + G[q][i] / alpha;
+            for (int i = 0; i < 4; ++i) G[q][i] = X[q][i] + div_by(G[q][i], alpha, 1.0f / alpha);
         }
         if (p.prox == LRS_PROX_SOFT) {
             const float T = (float)thr;
@@ -323,13 +531,13 @@ __global__ __launch_bounds__(256) void k_nlm_col(const float *__restrict__ g, in
     }
     __syncthreads();
     const double hh = hv ? hv[v] : h;
-    const double inv2 = 2.0 / ((hh * hh) * 9.0);
+    const double kneg = nlm_kneg(hh);
     const double c0 = nlm_c0();
     for (int i = threadIdx.x; i < K; i += blockDim.x) {
         double w[11];
 #pragma unroll
         for (int k = 0; k < 11; ++k) w[k] = (double)col[i + 5 - 3 + k];
-        out[v * ldo + i] = nlm_point<3>(w, inv2, c0);
+        out[v * ldo + i] = nlm_point<3>(w, kneg, c0);
     }
 }
 
@@ -350,8 +558,10 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
     dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));
     hipStream_t st = (hipStream_t)stream;
-    if (n_pad <= kStageRows)
-        hipLaunchKernelGGL((k_ista<256, true>), grid, dim3(kIstaThreads), 0, st, p);
+    if (n_pad <= kStageRows && prox == LRS_PROX_SOFT)
+        hipLaunchKernelGGL((k_ista_res<256, true>), grid, dim3(kIstaThreads), 0, st, p);
+    else if (n_pad <= kStageRows)
+        hipLaunchKernelGGL((k_ista_res<256, false>), grid, dim3(kIstaThreads), 0, st, p);
     else
         hipLaunchKernelGGL((k_ista<256, false>), grid, dim3(kIstaThreads), 0, st, p);
     LRS_CHECK_LAUNCH();
@@ -367,6 +577,22 @@ extern "C" int lrs_nlm_col_f32(const float *g, int64_t ldg, float *out, int64_t 
     if (nvec == 0) return LRS_OK;
     hipLaunchKernelGGL(k_nlm_col, dim3((unsigned)nvec), dim3(256), (size_t)(K + 10) * sizeof(float),
                        (hipStream_t)stream, g, ldg, out, ldo, (int)K, h, h_per_vec);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+// Diagnostic entry (not in include/lrspnp.h): time ablated variants of the resident kernel.
+extern "C" int lrs_diag_ista_ablate_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,
+                                        int64_t nb, const float *alpha, const double *thr, int Nit, int ablate,
+                                        float *phi, void *stream) {
+    if (n_pad > kStageRows || !phi) return LRS_E_INVALID;
+    IstaParams p{Yb, obs, D, alpha, thr, nullptr, phi, (int)n, (int)n_pad, Nit, LRS_PROX_NLM, nb};
+    const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
+    dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));
+    hipStream_t st = (hipStream_t)stream;
+    if (ablate == 1) hipLaunchKernelGGL((k_ista_res<256, false, 1>), grid, dim3(kIstaThreads), 0, st, p);
+    else if (ablate == 2) hipLaunchKernelGGL((k_ista_res<256, false, 2>), grid, dim3(kIstaThreads), 0, st, p);
+    else hipLaunchKernelGGL((k_ista_res<256, false, 0>), grid, dim3(kIstaThreads), 0, st, p);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }

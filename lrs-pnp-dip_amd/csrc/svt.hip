@@ -72,6 +72,14 @@ static size_t svt_ws_bytes(int64_t P, int64_t B) {
     return (size_t)((char *)(w.E + B * B) - (char *)nullptr) + 256;
 }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt) but not
+// for its outstanding global stores (the rotation log), unlike __syncthreads().
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Round-robin (circle method) pair k of round r over indices 0..Bp-1, returned with p < q.
 __device__ __forceinline__ void rr_pair(int r, int k, int Bp, int &p, int &q) {
     if (k == 0) { p = Bp - 1; q = r; }
@@ -198,7 +206,9 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
     double *A = sm;                      // packed upper triangle
     double *rc = A + npk, *rs = rc + half, *red = rs + half;
     int *ip = (int *)(red + 16), *iq = ip + half, *rowoff = iq + half;
+    __shared__ int any_rot;
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
     const bool use_warm = warm && w.state[0] == 1;
     const double *src = use_warm ? w.A0 : w.G;
     for (int i = tid; i < Bp; i += kJacobiThreads) rowoff[i] = i * Bp - (i * (i - 1)) / 2 - i;
@@ -206,33 +216,25 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
     for (int i = 0; i < Bp; ++i)
         for (int j = i + tid; j < Bp; j += kJacobiThreads) A[rowoff[i] + j] = src[(int64_t)i * Bp + j];
     __syncthreads();
-    auto norms = [&](double &dn, double &of) {
-        double d2 = 0.0, o2 = 0.0;
-        for (int i = 0; i < Bp; ++i)
-            for (int j = i + tid; j < Bp; j += kJacobiThreads) {
-                const double v = A[rowoff[i] + j];
-                if (i == j) d2 += v * v; else o2 += 2.0 * v * v;
-            }
-        dn = wg_reduce(d2, red);
-        of = wg_reduce(o2, red);
-    };
-    double dn, of;
-    norms(dn, of);
     int sweeps = 0, rounds = 0;
-    const double tol2 = 1e-26;   // off(A) <= 1e-13 ||A||
-    const int a0 = tid >> 5, b0 = tid & 31;
-    while (sweeps < kMaxSweeps && of > tol2 * (dn + of)) {
+    // threshold Jacobi: rotate (p,q) only while |a_pq| > tol * sqrt(|a_pp a_qq|); a sweep without
+    // any rotation ends the solve (the off-diagonal mass is then below tol relative).
+    const double tol = 1e-7;    // residual a_pq perturbs E = f(A) by ~|a_pq| f'(lambda): << 1e-8 relative in U
+    while (sweeps < kMaxSweeps) {
+        if (tid == 0) any_rot = 0;
+        lds_barrier();
         for (int r = 0; r < Bp - 1; ++r) {
             if (tid < half) {
                 int p, q;
                 rr_pair(r, tid, Bp, p, q);
                 const double app = A[rowoff[p] + p], aqq = A[rowoff[q] + q], apq = A[rowoff[p] + q];
                 double c = 1.0, s = 0.0;
-                if (apq != 0.0) {
+                if (fabs(apq) > tol * sqrt(fabs(app * aqq)) && apq != 0.0) {
                     const double theta = (aqq - app) / (2.0 * apq);
                     const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                     c = 1.0 / sqrt(t * t + 1.0);
                     s = t * c;
+                    any_rot = 1;
                 }
                 ip[tid] = p;
                 iq[tid] = q;
@@ -242,15 +244,17 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
                 log[0] = c;
                 log[1] = s;
             }
-            __syncthreads();
-            // A <- J^T A J on every unordered 2x2 block (k1 <= k2); J = [[c, s], [-s, c]] on (p, q)
-            for (int k1 = a0; k1 < half; k1 += 32) {
-                const int p1 = ip[k1], q1 = iq[k1];
+            lds_barrier();
+            // A <- J^T A J on every unordered 2x2 block (k1 <= k2); J = [[c, s], [-s, c]] on (p, q).
+            // One wave per k1 (wave-uniform rotation), lanes over k2; identity pairs are skipped.
+            for (int k1 = wv; k1 < half; k1 += kJacobiThreads / 64) {
                 const double c1 = rc[k1], s1 = rs[k1];
+                const bool id1 = (s1 == 0.0);
+                const int p1 = ip[k1], q1 = iq[k1];
                 const int ro_p1 = rowoff[p1], ro_q1 = rowoff[q1];
-                for (int k2 = b0; k2 < half; k2 += 32) {
-                    if (k2 < k1) continue;
+                for (int k2 = k1 + lane; k2 < half; k2 += 64) {
                     const double c2 = rc[k2], s2 = rs[k2];
+                    if (id1 && s2 == 0.0) continue;
                     if (k1 == k2) {
                         const int ipp = ro_p1 + p1, iqq = ro_q1 + q1, ipq = ro_p1 + q1;
                         const double a = A[ipp], b = A[ipq], d = A[iqq];
@@ -275,11 +279,13 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
                     }
                 }
             }
-            __syncthreads();
+            lds_barrier();
             ++rounds;
         }
         ++sweeps;
-        norms(dn, of);
+        const int rotated = any_rot;
+        lds_barrier();   // every thread has read the flag before thread 0 resets it
+        if (!rotated) break;
     }
     for (int i = tid; i < Bp; i += kJacobiThreads) w.lam[i] = A[rowoff[i] + i];
     if (tid == 0) {
@@ -289,13 +295,17 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
 }
 
 // ---- 4. V_new = V_old J_1 ... J_R, 64 rows per 1024-thread workgroup, rows in LDS ------------
+// The rotation log is staged kLogRounds rounds at a time (one global-latency per batch); rounds
+// are separated by LDS-only barriers.
 constexpr int kVRows = 64;
+constexpr int kLogRounds = 16;
 
 __global__ __launch_bounds__(1024) void k_jacobi_vrebuild(SvtWs w, int warm) {
-    extern __shared__ double vrow[];               // [kVRows][Bp]
-    __shared__ double lc[kMaxBp / 2], ls[kMaxBp / 2];
-    __shared__ int lp[kMaxBp / 2], lq[kMaxBp / 2];
+    extern __shared__ double vsm[];
     const int Bp = (int)w.Bp, half = Bp / 2;
+    double *vrow = vsm;                                   // [kVRows][Bp]
+    double *lcs = vrow + kVRows * Bp;                     // [kLogRounds][half][2]
+    short *lpq = (short *)(lcs + kLogRounds * half * 2);  // [kLogRounds][half][2]
     const int i0 = blockIdx.x * kVRows;
     const int nrows = min(kVRows, Bp - i0);
     const bool use_warm = warm && w.state[0] == 1;
@@ -308,27 +318,35 @@ __global__ __launch_bounds__(1024) void k_jacobi_vrebuild(SvtWs w, int warm) {
     }
     const int rounds = w.state[2];
     const int rr = threadIdx.x >> 4, kk = threadIdx.x & 15;
-    for (int rd = 0; rd < rounds; ++rd) {
+    for (int rb = 0; rb < rounds; rb += kLogRounds) {
+        const int nr = min(kLogRounds, rounds - rb);
         __syncthreads();
-        if (threadIdx.x < half) {
+        for (int idx = threadIdx.x; idx < nr * half; idx += 1024) {
+            const int ro = idx / half, k = idx % half;
+            const double *log = w.rot + ((int64_t)(rb + ro) * half + k) * 2;
+            lcs[2 * idx] = log[0];
+            lcs[2 * idx + 1] = log[1];
             int p, q;
-            rr_pair(rd % (Bp - 1), threadIdx.x, Bp, p, q);
-            const double *log = w.rot + ((int64_t)rd * half + threadIdx.x) * 2;
-            lp[threadIdx.x] = p;
-            lq[threadIdx.x] = q;
-            lc[threadIdx.x] = log[0];
-            ls[threadIdx.x] = log[1];
+            rr_pair((rb + ro) % (Bp - 1), k, Bp, p, q);
+            lpq[2 * idx] = (short)p;
+            lpq[2 * idx + 1] = (short)q;
         }
         __syncthreads();
-        if (rr < nrows) {
-            double *row = vrow + rr * Bp;
-            for (int k = kk; k < half; k += 16) {
-                const int p = lp[k], q = lq[k];
-                const double c = lc[k], s = ls[k];
-                const double vp = row[p], vq = row[q];
-                row[p] = c * vp - s * vq;
-                row[q] = s * vp + c * vq;
+        for (int ro = 0; ro < nr; ++ro) {
+            if (rr < nrows) {
+                double *row = vrow + rr * Bp;
+                for (int k = kk; k < half; k += 16) {
+                    const int e = ro * half + k;
+                    const double sn = lcs[2 * e + 1];
+                    if (sn == 0.0) continue;
+                    const double c = lcs[2 * e];
+                    const int p = lpq[2 * e], q = lpq[2 * e + 1];
+                    const double vp = row[p], vq = row[q];
+                    row[p] = c * vp - sn * vq;
+                    row[q] = sn * vp + c * vq;
+                }
             }
+            lds_barrier();
         }
     }
     __syncthreads();
@@ -456,9 +474,10 @@ extern "C" size_t lrs_svt_workspace(int64_t P, int64_t B) {
     return svt_ws_bytes(P, B);
 }
 
-extern "C" int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau, float *U,
-                           double *s_out, int warm, void *ws, size_t ws_bytes, void *stream) {
-    if (!X || !U || !ws || P <= 0 || B <= 0 || tau < 0.0) return LRS_E_INVALID;
+// Stage 1 (multi-workgroup, ~0.3 ms): fp64 Gram and, when warm, A0 = V^T G V.
+extern "C" int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, int warm, void *ws,
+                                size_t ws_bytes, void *stream) {
+    if (!X || !ws || P <= 0 || B <= 0) return LRS_E_INVALID;
     if (B + (B & 1) > kMaxBp) return LRS_E_UNSUPPORTED;
     if (ws_bytes < svt_ws_bytes(P, B)) return LRS_E_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
@@ -477,16 +496,28 @@ extern "C" int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P,
                        w.partial, w.nslab, (int)w.ntp, nt, (int)B, Bp, w.G);
     LRS_CHECK_LAUNCH();
     if (warm) {
-        // A0 = V^T (G V) with the current V (no-op result if V is not valid yet: the Jacobi
-        // kernel then starts from G)
+        // A0 = V^T (G V) with the current V (unused when V is not valid yet: Jacobi starts from G)
         const dim3 g16((Bp + 15) / 16, (Bp + 15) / 16);
         hipLaunchKernelGGL(k_gemm_f64_state, g16, dim3(256), 0, st, w, 0);
         LRS_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_gemm_f64_state, g16, dim3(256), 0, st, w, 1);
         LRS_CHECK_LAUNCH();
     }
+    return LRS_OK;
+}
+
+// Stage 2: one-workgroup Jacobi (runs beside the sparse-coding kernel), V replay, E, U.
+extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau,
+                                  float *U, double *s_out, int warm, void *ws, size_t ws_bytes, void *stream) {
+    if (!X || !U || !ws || P <= 0 || B <= 0 || tau < 0.0) return LRS_E_INVALID;
+    if (B + (B & 1) > kMaxBp) return LRS_E_UNSUPPORTED;
+    if (ws_bytes < svt_ws_bytes(P, B)) return LRS_E_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    SvtWs w = svt_ws_layout(ws, P, B);
+    const int Bp = (int)w.Bp;
     const size_t smem = sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp + 16) + sizeof(int) * (2 * Bp);
-    const size_t vsmem = sizeof(double) * (size_t)kVRows * Bp;
+    const size_t vsmem = sizeof(double) * ((size_t)kVRows * Bp + (size_t)kLogRounds * (Bp / 2) * 2) +
+                         sizeof(short) * (size_t)kLogRounds * (Bp / 2) * 2;
     // dynamic LDS above 64 KiB must be opted into; request exactly what this shape needs
     hipError_t ea = hipFuncSetAttribute((const void *)k_jacobi_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)smem);
@@ -511,4 +542,18 @@ extern "C" int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P,
     hipLaunchKernelGGL(k_svt_apply, grid, dim3(256), 0, st, X, L2, c2, w.E, P, (int)B, U);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
+}
+
+extern "C" int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau, float *U,
+                           double *s_out, int warm, void *ws, size_t ws_bytes, void *stream) {
+    if (!U || tau < 0.0) return LRS_E_INVALID;
+    int rc = lrs_svt_gram_f32(X, L2, c2, P, B, warm, ws, ws_bytes, stream);
+    if (rc != LRS_OK) return rc;
+    return lrs_svt_finish_f32(X, L2, c2, P, B, tau, U, s_out, warm, ws, ws_bytes, stream);
+}
+
+// Diagnostics (not in include/lrspnp.h): Jacobi rounds / sweeps of the last call (host copy).
+extern "C" int lrs_diag_svt_state(void *ws, int64_t P, int64_t B, int *out4) {
+    SvtWs w = svt_ws_layout(ws, P, B);
+    return (int)hipMemcpy(out4, w.state, 4 * sizeof(int), hipMemcpyDeviceToHost);
 }

@@ -155,6 +155,30 @@ def svt(X, L2, c2: float, tau: float, ws, U=None, s_out=None, warm=False, stream
     return U
 
 
+def svt_gram(X, L2, c2: float, ws, warm=False, stream=None):
+    """First half of svt(): fp64 Gram (+ warm-start product), multi-workgroup."""
+    L = device_lib()
+    P, B = X.shape
+    check(L.lrs_svt_gram_f32(_p(X), _p(L2), float(c2), P, B, int(bool(warm)), _p(ws), ws.numel(), _s(stream)),
+          "lrs_svt_gram_f32")
+
+
+def svt_finish(X, L2, c2: float, tau: float, ws, U, s_out=None, warm=False, stream=None):
+    """Second half of svt(): one-workgroup Jacobi, V update, U = Z - Z E."""
+    L = device_lib()
+    P, B = X.shape
+    check(L.lrs_svt_finish_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out), int(bool(warm)),
+                               _p(ws), ws.numel(), _s(stream)), "lrs_svt_finish_f32")
+    return U
+
+
+def svt_state(ws, P: int, B: int):
+    """(V valid, V buffer, Jacobi rounds, sweeps) of the last SVT call (diagnostics; syncs)."""
+    out = (ctypes.c_int * 4)()
+    check(device_lib().lrs_diag_svt_state(_p(ws), P, B, ctypes.cast(out, ctypes.c_void_p)), "lrs_diag_svt_state")
+    return list(out)
+
+
 def admm_update(X, L1, L2, Y, M, U, phi, bb, grid, gamma, mu1, mu2, norms=None, imout=None, stream=None):
     """In-place col2im + X update + dual updates (main_LRS_PnP.py:324-362)."""
     L = device_lib()

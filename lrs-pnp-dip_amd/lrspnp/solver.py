@@ -126,9 +126,18 @@ class LrsPnP:
         """One outer ADMM iteration (main_LRS_PnP.py:250-366), stream-ordered, no host sync."""
         main = torch.cuda.current_stream()
         lr = self.lowrank_stream
+        warm = self.cfg.svt_warm and self.iteration > 0
         lr.wait_stream(main)
-        self.low_rank(stream=lr)          # queued first: its Gram kernels grab the chip briefly,
-        self.sparse_coding(stream=main)   # then the one-workgroup eigensolver runs beside ISTA
+        # low-rank prox, first half (whole chip, ~0.3 ms): fp64 Gram + warm-start products
+        ops.svt_gram(self.X, self.L2, self.c2, self.svt_ws, warm=warm, stream=lr)
+        gram_done = lr.record_event()
+        # second half: the one-workgroup eigensolver then runs beside the sparse coding
+        ops.svt_finish(self.X, self.L2, self.c2, self.tau, self.svt_ws, self.U, warm=warm, stream=lr)
+        ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
+                   stream=main)
+        main.wait_event(gram_done)
+        ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
+                 stream=main)
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
                         self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)

@@ -126,9 +126,12 @@ int oracle_nlm_fast2d(const float *img, int H, int W, int C, int s, int d, doubl
  * all 11 padded columns are equal, the integral-image window degenerates to rows p..p+1 and the
  * 28 shifts fold into
  *     out[i] = (8 w0 v[p] + 7 sum_t w(p,t) v[p+t]) / (8 w0 + 7 sum_t w(p,t)),   t = +-1,+-2,+-3
- * with D(p,t) = [(v[p]-v[p+t])^2 + (v[p+1]-v[p+1+t])^2] * (2 / (9 h^2)), w = fast_exp(-D) unless
- * D > 5.  This is the CANONICAL evaluation order the HIP kernels reproduce bit-for-bit
- * (csrc/lrs_nlm.h): sums in t = -3..3 order, fma for the weighted sums, one double division.
+ * with distance D(p,t) = [(v[p]-v[p+t])^2 + (v[p+1]-v[p+1+t])^2] * 2/(9 h^2) and
+ * w = fast_exp(-D) unless D > 5.  CANONICAL evaluation order, reproduced bit-for-bit by the HIP
+ * kernels (csrc/lrs_nlm.h): the Schraudolph scale is folded into the normaliser,
+ *     y = S * kneg,  kneg = -1512775.3951951856938 * (2/((h*h)*9)),  skip if y < -1512775.39..*5,
+ *     w = double{hi = (int)y + 1072632447, lo = 0},
+ * sums in t = -3..3 order, fma for the weighted sums, one double division.
  * Against skimage's integral-image loop it differs only through rounding of D and of the double
  * accumulators (<= 1 ulp of the float32 output, ~1e-5 of elements; tests/test_oracle.py).
  * g: K floats with stride `ldg`; out: K floats with stride `ldo`.
@@ -138,7 +141,9 @@ void oracle_nlm_col(const float *g, long K, long ldg, double h, float *out, long
     const long n = K + 2 * pad;
     double *v = (double *)malloc(sizeof(double) * (size_t)n);
     for (long i = 0; i < n; ++i) v[i] = (double)g[reflect_idx((int)(i - pad), (int)K) * ldg];
-    const double inv2 = 2.0 / ((h * h) * 9.0);
+    const double A = 1512775.3951951856938;
+    const double kneg = -A * (2.0 / ((h * h) * 9.0));
+    const double ycut = -A * 5.0;
     const double c0 = 8.0 * fast_exp(-0.0);
     for (long i = 0; i < K; ++i) {
         long p = i + pad;
@@ -147,9 +152,13 @@ void oracle_nlm_col(const float *g, long K, long ldg, double h, float *out, long
             if (t == 0) continue;
             double a = v[p] - v[p + t], b = v[p + 1] - v[p + 1 + t];
             double aa = a * a, bb = b * b;
-            double D = (aa + bb) * inv2;
-            if (D > NLM_DISTANCE_CUTOFF) continue;
-            double w = fast_exp(-D);
+            double y = (aa + bb) * kneg;
+            double w = 0.0;
+            if (!(y < ycut)) {
+                int32_t hi = (int32_t)y + 1072632447;
+                uint64_t bits = ((uint64_t)(uint32_t)hi) << 32;
+                memcpy(&w, &bits, sizeof w);
+            }
             sw = sw + w;
             swv = fma(w, v[p + t], swv);
         }
