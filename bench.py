@@ -108,33 +108,26 @@ def cpu_baseline(Y, M, D, bb, nit, budget_s):
 def main():
     args = parse()
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    from lrspnp import dist as D
+    ctx = D.init_from_env("nccl")
     from lrspnp import LrsPnP, LrsPnPConfig, ops
     from lrspnp.metrics import mpsnr
 
     H, W, B = (int(v) for v in args.cube.split("x"))
-    Y, M, D, clean = make_problem(H, W, B, args.bb, args.K, seed=rank)
+    Y, M, Dct, clean = make_problem(H, W, B, args.bb, args.K, seed=ctx.rank)   # one cube per rank
     cfg = LrsPnPConfig(bb=args.bb, sliding=args.bb, Nit=args.nit, variant="spec2")
     t0 = time.perf_counter()
-    s = LrsPnP(Y, M, D, cfg)
+    s = LrsPnP(Y, M, Dct, cfg)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
     clean_d = torch.from_numpy(clean).cuda()
     mp0 = mpsnr(s.X, clean_d)
 
     # dominant-kernel timing: HIP events on the stream the ISTA kernel is launched on
-    main_stream = torch.cuda.current_stream()
     ev = []
     orig_ista = ops.ista
+    timing = [False]
 
     def timed_ista(*a, **k):
         st = k.get("stream") or torch.cuda.current_stream()
@@ -143,32 +136,25 @@ def main():
         e0.record(st)
         out = orig_ista(*a, **k)
         e1.record(st)
-        ev.append((e0, e1))
+        if timing[0]:
+            ev.append((e0, e1))
         return out
 
-    import lrspnp.solver as solver_mod
-    solver_mod.ops.ista = timed_ista
-    for _ in range(args.warmup):
+    ops.ista = timed_ista
+
+    def step():
+        if not timing[0] and warm_done[0] >= args.warmup:
+            timing[0] = True
+        warm_done[0] += 1
         s.step()
-    torch.cuda.synchronize()
-    ev.clear()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        s.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    solver_mod.ops.ista = orig_ista
+
+    warm_done = [0]
+    elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
+    ops.ista = orig_ista
     ista_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     mp1 = mpsnr(s.X, clean_d)
+    world, rank = ctx.world, ctx.rank
+    mps = D.gather_scalars([mp0, mp1], ctx)
 
     n, K, nb = args.bb * args.bb, args.K, s.nb
     flops = args.nit * nb * 4 * n * K + nb * 2 * n * K
@@ -200,14 +186,16 @@ def main():
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                      "traffic": traffic, "flops_per_launch": flops, "ms_per_launch": ista_ms},
         "setup_s": setup_s,
-        "mpsnr": {"input": mp0, "after_steps": mp1, "steps_run": args.warmup + args.steps},
+        "mpsnr": {"input": mp0, "after_steps": mp1, "steps_run": args.warmup + args.steps,
+                  "per_rank": mps},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(Y, M, D, args.bb, args.nit, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(Y, M, Dct, args.bb, args.nit, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
 
 
 if __name__ == "__main__":

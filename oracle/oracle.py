@@ -137,6 +137,9 @@ def ista_alpha_h(H: np.ndarray, lambda_ista: float, variant: str):
     variant 'soft'  : ista.m:15-23                 alpha = ||H||_2^2, soft threshold T
     """
     H = np.asarray(H, dtype=np.float32)
+    if H.shape[0] == 0:
+        # no observed row: the reference divides by alpha = 0 (undefined); lrspnp's convention
+        return np.float32(1.0), 1.0
     if variant in ("spec2", "soft"):
         alpha = np.linalg.norm(H, 2) ** 2
     elif variant == "fro4":
