@@ -125,6 +125,111 @@ int lrs_admm_update_f32(float *X, float *L1, float *L2, const float *Y, const fl
                         const int32_t *chi, float gamma, float mu1, float mu2, double *norms,
                         float *imout, void *stream);
 
+/* ==== DIP low-rank prox (the 1-Lipschitz U-Net of main_LRS_PnP_DIP_1-LiP.py) ================
+ * Activations are [C][H][W] float32 (batch 1).  Reference interfaces replaced:
+ *   lrs_conv2d_*        ReflectionPad2d + Conv2d + nn.Upsample(x2, nearest)
+ *                       (models/lipschitz_constraint_layer.py:65-78, my_Lipschitz_Unet.py:71-94)
+ *   lrs_bn_act_*        BatchNormSpectralNorm-wrapped BatchNorm2d (train mode) + LeakyReLU(0.2)
+ *                       (lipschitz_constraint_layer.py:88-122,154-159, 6-22)
+ *   lrs_sigma_max_f32   SpectralNorm._update_u_v: torch.svd(W.view(Co,-1))[0]  (:36-44)
+ *   lrs_adam_f32        torch.optim.Adam(lr) step                      (…1-LiP.py:215,237)
+ *   lrs_masked_mse_f32  MSELoss(target*mask, out*mask) + its gradient  (…1-LiP.py:216,234)
+ *   lrs_es_*            EarlyStop / myMetric variance test             (…1-LiP.py:71-103,244-264)
+ *   lrs_dipnet_*        my_Lipschitz_Unet + the get_DIP_out training loop (…1-LiP.py:208-264) */
+#define LRS_PAD_ZERO 0
+#define LRS_PAD_REFLECT 1
+#define LRS_ACT_NONE 0
+#define LRS_ACT_LRELU 1   /* LeakyReLU(0.2) */
+#define LRS_ACT_SIGMOID 2
+
+/* Output size of the conv unit (upsample, pad, k, stride). */
+int lrs_conv2d_out_size(int H, int W, int k, int stride, int pad, int upsample, int *Ho, int *Wo);
+/* col workspace (floats) for lrs_conv2d_fwd_f32: Cin*k*k*Ho*Wo (0 when the unit is a plain 1x1). */
+int64_t lrs_conv2d_col_size(int Cin, int H, int W, int k, int stride, int pad, int upsample);
+/* y[Cout][Ho][Wo] = conv(pad(upsample(x))) + bias.  col receives the im2col matrix (kept for
+ * the backward); ws/ws_bytes: split-K partials (lrs_conv2d_workspace). */
+size_t lrs_conv2d_workspace(int Cin, int H, int W, int Cout, int k, int stride, int pad, int upsample);
+int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const float *w, const float *bias,
+                       int Cout, int k, int stride, int pad, int pad_mode, int upsample, float *col,
+                       float *y, void *ws, size_t ws_bytes, void *stream);
+/* gw = (gy col^T) / *w_div (w_div nullable, device scalar: the spectral-norm scale);
+ * gx (nullable) = adjoint of the im2col of gy through w.  gbias is produced by lrs_bn_act_bwd.
+ * col = the forward's col (or x itself for a plain 1x1 unit). */
+int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float *w, const float *w_div, int Cin,
+                       int H, int W, int Cout, int k, int stride, int pad, int pad_mode, int upsample,
+                       float *gx, float *gw, void *ws, size_t ws_bytes, void *stream);
+
+/* y = act(BN_lip(z)) with batch statistics (gamma == NULL: y = act(z)).  Saves mean / invstd
+ * [C]; running stats (nullable) get the momentum update. */
+int lrs_bn_act_fwd_f32(const float *z, float *y, const float *gamma, const float *beta, float *mean,
+                       float *invstd, float *run_mean, float *run_var, int C, int64_t P, int act,
+                       float eps, float momentum, void *stream);
+int lrs_bn_act_bwd_f32(const float *gy, const float *y, const float *z, const float *gamma,
+                       const float *mean, const float *invstd, float *gz, float *ggamma,
+                       float *gbeta, float *gbias, int C, int64_t P, int act, void *stream);
+
+/* sigma_max of n weight matrices W[i] (rows[i] x cols[i], min(rows, cols) <= 128; host arrays
+ * of device pointers), exact to fp64 before the float32 rounding; scale = max(1, sigma/ln_lambda)
+ * and, when Wn != NULL, Wn[i] = W[i] / scale[i]. */
+size_t lrs_sigma_max_workspace(int n);
+int lrs_sigma_max_f32(const float *const *W, float *const *Wn, const int *rows, const int *cols, int n,
+                      float ln_lambda, float *sigma, float *scale, void *ws, size_t ws_bytes,
+                      void *stream);
+
+/* One Adam step over a flat buffer; step (device int) is the 1-based step count. */
+int lrs_adam_f32(float *p, const float *g, float *m, float *v, int64_t n, const int *step, float lr,
+                 float beta1, float beta2, float eps, void *stream);
+/* loss_acc (device double) += sum((target*mask - out*mask)^2); gout (nullable) = dL/dout of the
+ * mean.  mask (nullable) is [P], broadcast over the C channels. */
+int lrs_masked_mse_f32(const float *out, const float *target, const float *mask, int C, int64_t P,
+                       float *gout, double *loss_acc, void *stream);
+
+/* Early stopping state (device memory).  lrs_es_init fills it; every lrs_es_update_f32 pushes one
+ * output into the ring [size][N] and, once full, applies the variance test. */
+typedef struct {
+    int32_t count, size, patience, wait, stop, stop_epoch, best_epoch, reserved;
+    double best, var_acc, last_var;
+} lrs_es_state;
+int lrs_es_init(lrs_es_state *st, int size, int patience, void *stream);
+int lrs_es_update_f32(const float *out, int64_t N, float *ring, lrs_es_state *st, void *stream);
+
+/* ---- Whole network + training step ---------------------------------------------------------
+ * A sequential stack of conv units (the 1-Lip U-Net is one).  The host object holds shapes and
+ * offsets only; parameters, gradients, Adam moments and the workspace are caller-owned device
+ * buffers given to lrs_dipnet_bind. */
+typedef struct {
+    int32_t cin, cout, k, stride, pad, pad_mode, upsample, bn, act;
+} lrs_conv_unit;
+typedef struct lrs_dipnet lrs_dipnet;
+int lrs_dipnet_create(const lrs_conv_unit *units, int n_units, int H, int W, lrs_dipnet **out);
+void lrs_dipnet_destroy(lrs_dipnet *net);
+int64_t lrs_dipnet_num_params(const lrs_dipnet *net);
+int64_t lrs_dipnet_num_bnstats(const lrs_dipnet *net);
+size_t lrs_dipnet_workspace(const lrs_dipnet *net);
+/* offsets (floats) of unit i's parameters in the flat buffer; -1 when absent */
+int lrs_dipnet_param_offsets(const lrs_dipnet *net, int unit, int64_t *w, int64_t *b, int64_t *gamma,
+                             int64_t *beta);
+int lrs_dipnet_out_shape(const lrs_dipnet *net, int *C, int *H, int *W);
+int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, float *adam_m, float *adam_v,
+                    float *bnstats, void *ws, size_t ws_bytes);
+/* Kaiming-uniform(a=0, fan_in) conv weights, torch-default biases, gamma = 1, beta = 0, zero Adam
+ * state; a counter-based RNG keyed by seed (the reference draws from the unseeded torch RNG). */
+int lrs_dipnet_init_params(lrs_dipnet *net, uint64_t seed, void *stream);
+/* zero the Adam moments and the step count (a fresh optimizer on the current parameters) */
+int lrs_dipnet_reset_optimizer(lrs_dipnet *net, void *stream);
+/* forward only (spectral norms included); the output stays in lrs_dipnet_output() */
+int lrs_dipnet_forward(lrs_dipnet *net, const float *x, void *stream);
+const float *lrs_dipnet_output(const lrs_dipnet *net);
+const float *lrs_dipnet_grads(const lrs_dipnet *net);
+/* nsteps training steps: forward, masked MSE, backward, Adam; es (nullable) gets every step's
+ * forward output (ring: es->size * C*H*W floats).  use_graph != 0 captures one step into a
+ * hipGraph (on first use, re-captured when any argument changes) and replays it. */
+int lrs_dipnet_train_steps(lrs_dipnet *net, const float *x, const float *target, const float *mask,
+                           float lr, float beta1, float beta2, float eps, lrs_es_state *es,
+                           float *ring, int nsteps, int use_graph, void *stream);
+/* loss of the last step (synchronises the stream; diagnostics only) */
+int lrs_dipnet_last_loss(lrs_dipnet *net, double *loss, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,657 @@
+// DIP low-rank prox primitives: the layers of the 1-Lipschitz U-Net and its training step.
+//
+// Reference (shuoli0708/LRS-PnP-DIP):
+//   models/my_Lipschitz_Unet.py:21-148        the network (conv / bn / act stack)
+//   models/lipschitz_constraint_layer.py:6-22   act(): LeakyReLU(0.2, inplace=True)
+//   lipschitz_constraint_layer.py:36-44         SpectralNorm._update_u_v: sigma = svd(W.view(Co,-1))[0],
+//                                               W = W_bar / max(1, sigma / ln_lambda)
+//   lipschitz_constraint_layer.py:65-78         conv(): ReflectionPad2d((k-1)//2) + Conv2d(pad 0)
+//   lipschitz_constraint_layer.py:88-101,113-122  BatchNormSpectralNorm: gamma/c, beta/c with
+//                                               c = max(max|gamma_orig|, 1) (no grad through c)
+//   main_LRS_PnP_DIP_1-LiP.py:214-237           Adam(lr), MSELoss(target*mask, out*mask)
+//
+// MI355X design: activations are [C][H][W] fp32 (batch 1, as the reference).  A conv is an
+// explicit im2col (reflection pad / stride / nearest x2 upsample folded into the gather) and an
+// MFMA f32 GEMM; the backward is the same GEMM transposed (dW = dZ col^T with split-K, dcol =
+// Wn^T dZ) plus a deterministic col2im gather that also applies the adjoints of the padding and
+// the upsample.  BatchNorm (train-mode batch statistics) + LeakyReLU are one kernel per
+// direction, one workgroup per channel, statistics in fp64.  sigma_max of every conv weight is
+// computed exactly (not by power iteration): fp64 Gram on the smaller side, then Lanczos with
+// the Gram held in registers and a 256-way parallel Sturm multisection for the top eigenvalue.
+#include <math.h>
+
+#include "lrs_common.h"
+#include "lrs_dip.h"
+
+// Kernel definitions; included by dipnet.hip only (one translation unit).
+#pragma once
+
+namespace lrs {
+
+// ------------------------------------------------------------------------------------------
+// GEMM  C[M][N] = op(A)[M][K] * op(B)[K][N]   (fp32, v_mfma_f32_16x16x4_f32)
+//   TA = 0: A stored [M][K];  TA = 1: A stored [K][M]
+//   TB = 0: B stored [K][N];  TB = 1: B stored [N][K]
+// 64x64 tile per 256-thread workgroup, BK = 16, each wave a 32x32 sub-tile (2x2 MFMA tiles).
+// gridDim.z > 1 = split-K: partial z goes to Cpart + z*M*N and k_gemm_reduce finishes.
+// ------------------------------------------------------------------------------------------
+constexpr int kBM = 64, kBN = 64, kBK = 16, kGemmThreads = 256;
+
+struct GemmArgs {
+    const float *A, *B;
+    float *C;            // final output (split == 1) or partial base (split > 1)
+    const float *bias;   // [M] or null (split == 1 only)
+    const float *div;    // scalar divisor (device) or null (split == 1 only)
+    int M, N, K, kchunk;
+};
+
+// Load a 16(k) x 64(x) operand tile into 4 registers per thread.
+//  kmajor = stored [k][x] (contiguous along x), else stored [x][k] (contiguous along k).
+template <bool KMAJOR>
+__device__ __forceinline__ void load_tile(const float *__restrict__ S, int ld, int k0, int kend, int x0, int X,
+                                          float (&r)[4]) {
+    const int t = threadIdx.x;
+    if (KMAJOR) {
+        const int kk = t >> 4, i = (t & 15) * 4;
+        const int k = k0 + kk;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int x = x0 + i + u;
+            r[u] = (k < kend && x < X) ? S[(int64_t)k * ld + x] : 0.0f;
+        }
+    } else {
+        const int i = t >> 2, kk = (t & 3) * 4;
+        const int x = x0 + i;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + kk + u;
+            r[u] = (k < kend && x < X) ? S[(int64_t)x * ld + k] : 0.0f;
+        }
+    }
+}
+
+template <bool KMAJOR>
+__device__ __forceinline__ void store_tile(float (*T)[kBM + 4], const float (&r)[4]) {
+    const int t = threadIdx.x;
+    if (KMAJOR) {
+        const int kk = t >> 4, i = (t & 15) * 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) T[kk][i + u] = r[u];
+    } else {
+        const int i = t >> 2, kk = (t & 3) * 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) T[kk + u][i] = r[u];
+    }
+}
+
+template <int TA, int TB>
+__global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
+    __shared__ float As[kBK][kBM + 4];
+    __shared__ float Bs[kBK][kBN + 4];
+    const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+    const int kbeg = blockIdx.z * g.kchunk;
+    const int kend = min(g.K, kbeg + g.kchunk);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wm = (wv >> 1) * 32, wn = (wv & 1) * 32;
+    const int jl = lane & 15, gk = lane >> 4;
+    // A: TA=0 stored [M][K] -> contiguous along k (x-major); TA=1 stored [K][M] (k-major)
+    const int lda = TA ? g.M : g.K;
+    const int ldb = TB ? g.K : g.N;
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float ra[4], rb[4];
+    load_tile<TA == 1>(g.A, lda, kbeg, kend, m0, g.M, ra);
+    load_tile<TB == 0>(g.B, ldb, kbeg, kend, n0, g.N, rb);
+    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+        store_tile<TA == 1>(As, ra);
+        store_tile<TB == 0>(Bs, rb);
+        __syncthreads();
+        if (k0 + kBK < kend) {
+            load_tile<TA == 1>(g.A, lda, k0 + kBK, kend, m0, g.M, ra);
+            load_tile<TB == 0>(g.B, ldb, k0 + kBK, kend, n0, g.N, rb);
+        }
+#pragma unroll
+        for (int s = 0; s < kBK / 4; ++s) {
+            const float a0 = As[4 * s + gk][wm + jl], a1 = As[4 * s + gk][wm + 16 + jl];
+            const float b0 = Bs[4 * s + gk][wn + jl], b1 = Bs[4 * s + gk][wn + 16 + jl];
+            acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
+            acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
+            acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
+            acc[1][1] = mfma16x16x4(a1, b1, acc[1][1]);
+        }
+        __syncthreads();
+    }
+    float *C = g.C + (int64_t)blockIdx.z * g.M * g.N;
+    const bool final_out = gridDim.z == 1;
+    const float dv = (final_out && g.div) ? *g.div : 1.0f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int n = n0 + wn + 16 * b + jl;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + 16 * a + 4 * gk + r;
+                if (m < g.M && n < g.N) {
+                    float v = acc[a][b][r];
+                    if (final_out) {
+                        if (g.bias) v = v + g.bias[m];
+                        if (g.div) v = v / dv;
+                    }
+                    C[(int64_t)m * g.N + n] = v;
+                }
+            }
+        }
+}
+
+// C = (sum_z part[z]) (+ bias[m]) (/ *div): fixed summation order (deterministic).
+__global__ void k_gemm_reduce(const float *__restrict__ part, int nsplit, int M, int N, const float *bias,
+                              const float *div, float *__restrict__ C) {
+    const int64_t MN = (int64_t)M * N;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= MN) return;
+    float s = part[i];
+    for (int z = 1; z < nsplit; ++z) s += part[(int64_t)z * MN + i];
+    if (bias) s = s + bias[i / N];
+    if (div) s = s / *div;
+    C[i] = s;
+}
+
+// ------------------------------------------------------------------------------------------
+// im2col / col2im with nearest x2 upsample and reflection / zero padding folded in.
+//   source x: [C][Hs][Ws];  upsampled (Hu, Wu) = up ? (2Hs, 2Ws) : (Hs, Ws);
+//   padded coordinate iy in [0, Hu + 2 pad);  col[(c*k + ky)*k + kx][oy*Wo + ox] =
+//   xsrc(c, iy = oy*stride + ky, ix = ox*stride + kx)   (torch weight order [co][ci][ky][kx])
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int reflect_idx(int u, int n) {   // ReflectionPad2d (no edge repeat)
+    if (u < 0) u = -u;
+    if (u >= n) u = 2 * (n - 1) - u;
+    return u;
+}
+
+__global__ void k_im2col(const float *__restrict__ x, ConvGeom gm, float *__restrict__ col) {
+    const int64_t P = (int64_t)gm.Ho * gm.Wo;
+    const int64_t total = (int64_t)gm.Cin * gm.k * gm.k * P;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / P;
+        const int p = (int)(i - r * P);
+        const int kx = (int)(r % gm.k), ky = (int)((r / gm.k) % gm.k), c = (int)(r / (gm.k * gm.k));
+        const int oy = p / gm.Wo, ox = p - oy * gm.Wo;
+        int uy = oy * gm.stride + ky - gm.pad, ux = ox * gm.stride + kx - gm.pad;
+        float v = 0.0f;
+        bool inside = true;
+        if (gm.pad_mode == LRS_PAD_REFLECT) {
+            uy = reflect_idx(uy, gm.Hu);
+            ux = reflect_idx(ux, gm.Wu);
+        } else {
+            inside = uy >= 0 && uy < gm.Hu && ux >= 0 && ux < gm.Wu;
+        }
+        if (inside) {
+            const int sy = gm.up ? (uy >> 1) : uy, sx = gm.up ? (ux >> 1) : ux;
+            v = x[((int64_t)c * gm.Hs + sy) * gm.Ws + sx];
+        }
+        col[i] = v;
+    }
+}
+
+// Padded positions that read upsampled index u (n = upsampled extent): the direct one and, for
+// reflection, the top/left mirror (u in [1, pad]) and the bottom/right mirror
+// (u in [n-1-pad, n-2]); a tiny extent can have all three.
+__device__ __forceinline__ int padded_sources(int u, int n, int pad, int mode, int (&iy)[3]) {
+    int cnt = 0;
+    iy[cnt++] = u + pad;
+    if (mode == LRS_PAD_REFLECT && pad > 0) {
+        if (u >= 1 && u <= pad) iy[cnt++] = pad - u;
+        if (u >= n - 1 - pad && u <= n - 2) iy[cnt++] = 2 * (n - 1) - u + pad;
+    }
+    return cnt;
+}
+
+// dx[c][y][x] = sum over every col entry that read it (adjoint of k_im2col), gather form.
+__global__ void k_col2im(const float *__restrict__ dcol, ConvGeom gm, float *__restrict__ dx) {
+    const int64_t total = (int64_t)gm.Cin * gm.Hs * gm.Ws;
+    const int64_t P = (int64_t)gm.Ho * gm.Wo;
+    const int k = gm.k, s = gm.stride;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int sx = (int)(i % gm.Ws), sy = (int)((i / gm.Ws) % gm.Hs), c = (int)(i / ((int64_t)gm.Ws * gm.Hs));
+        float acc = 0.0f;
+        const int nup = gm.up ? 2 : 1;
+        for (int a = 0; a < nup; ++a) {
+            const int uy = gm.up ? 2 * sy + a : sy;
+            int iys[3];
+            const int ny = padded_sources(uy, gm.Hu, gm.pad, gm.pad_mode, iys);
+            for (int b = 0; b < nup; ++b) {
+                const int ux = gm.up ? 2 * sx + b : sx;
+                int ixs[3];
+                const int nx = padded_sources(ux, gm.Wu, gm.pad, gm.pad_mode, ixs);
+                for (int py = 0; py < ny; ++py)
+                    for (int ky = 0; ky < k; ++ky) {
+                        const int ty = iys[py] - ky;
+                        if (ty < 0 || ty % s) continue;
+                        const int oy = ty / s;
+                        if (oy >= gm.Ho) continue;
+                        for (int px = 0; px < nx; ++px)
+                            for (int kx = 0; kx < k; ++kx) {
+                                const int tx = ixs[px] - kx;
+                                if (tx < 0 || tx % s) continue;
+                                const int ox = tx / s;
+                                if (ox >= gm.Wo) continue;
+                                acc += dcol[((int64_t)(c * k + ky) * k + kx) * P + (int64_t)oy * gm.Wo + ox];
+                            }
+                    }
+            }
+        }
+        dx[i] = acc;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm2d (train mode, batch 1) with the Lipschitz rescale, + LeakyReLU(0.2), fused.
+// One workgroup per channel; statistics in fp64 (two-pass).
+// ------------------------------------------------------------------------------------------
+constexpr int kBnThreads = 256;
+
+__device__ __forceinline__ double block_sum_d(double v, double *red) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+    return s;
+}
+
+// c = max(max|gamma_orig|, 1.0) (lipschitz_constraint_layer.py:93-97)
+__device__ float bn_lip_scale(const float *gamma, int C, double *red) {
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < C; i += blockDim.x) m = fmaxf(m, fabsf(gamma[i]));
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_down(m, off, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    float r = 0.0f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r = fmaxf(r, (float)red[i]);
+    __syncthreads();
+    return fmaxf(r, 1.0f);
+}
+
+__device__ __forceinline__ float act_fwd(float v, int act) {
+    if (act == LRS_ACT_LRELU) return v > 0.0f ? v : v * 0.2f;
+    if (act == LRS_ACT_SIGMOID) return 1.0f / (1.0f + expf(-v));
+    return v;
+}
+
+__device__ __forceinline__ float act_bwd(float g, float y, int act) {
+    if (act == LRS_ACT_LRELU) return y > 0.0f ? g : g * 0.2f;
+    if (act == LRS_ACT_SIGMOID) return g * (1.0f - y) * y;
+    return g;
+}
+
+struct BnArgs {
+    const float *z;          // [C][P] conv output
+    float *y;                // [C][P] activation output (may alias z when !bn)
+    const float *gamma, *beta;   // bn params (orig), null when !bn
+    float *mean, *invstd;    // [C] saved statistics
+    float *run_mean, *run_var;   // [C] running statistics (updated, momentum)
+    int C, P, bn, act;
+    float eps, momentum;
+};
+
+__global__ __launch_bounds__(kBnThreads) void k_bn_act_fwd(BnArgs a) {
+    __shared__ double red[kBnThreads / 64];
+    const int c = blockIdx.x;
+    const float *z = a.z + (int64_t)c * a.P;
+    float *y = a.y + (int64_t)c * a.P;
+    if (!a.bn) {
+        for (int i = threadIdx.x; i < a.P; i += blockDim.x) y[i] = act_fwd(z[i], a.act);
+        return;
+    }
+    const float cs = bn_lip_scale(a.gamma, a.C, red);
+    double s = 0.0;
+    for (int i = threadIdx.x; i < a.P; i += blockDim.x) s += (double)z[i];
+    const double mean = block_sum_d(s, red) / a.P;
+    double q = 0.0;
+    for (int i = threadIdx.x; i < a.P; i += blockDim.x) {
+        const double d = (double)z[i] - mean;
+        q += d * d;
+    }
+    const double var = block_sum_d(q, red) / a.P;
+    const float m32 = (float)mean;
+    const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
+    const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
+    for (int i = threadIdx.x; i < a.P; i += blockDim.x) y[i] = act_fwd((z[i] - m32) * is32 * gm + bt, a.act);
+    if (threadIdx.x == 0) {
+        a.mean[c] = m32;
+        a.invstd[c] = is32;
+        if (a.run_mean) {
+            const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
+            a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
+            a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+        }
+    }
+}
+
+struct BnBwdArgs {
+    const float *gy;         // [C][P] dL/dy
+    const float *y, *z;      // activation output, conv output
+    const float *gamma;      // bn gamma_orig (null when !bn)
+    const float *mean, *invstd;
+    float *gz;               // [C][P] dL/dz (may alias gy)
+    float *ggamma, *gbeta;   // [C] grads of gamma_orig / beta_orig (null when !bn)
+    float *gbias;            // [C] grad of the conv bias = sum_p dL/dz
+    int C, P, bn, act;
+};
+
+__global__ __launch_bounds__(kBnThreads) void k_bn_act_bwd(BnBwdArgs a) {
+    __shared__ double red[kBnThreads / 64];
+    const int c = blockIdx.x;
+    const int64_t off = (int64_t)c * a.P;
+    const float *gy = a.gy + off, *y = a.y + off, *z = a.z + off;
+    float *gz = a.gz + off;
+    if (!a.bn) {
+        double s = 0.0;
+        for (int i = threadIdx.x; i < a.P; i += blockDim.x) {
+            const float g = act_bwd(gy[i], y[i], a.act);
+            gz[i] = g;
+            s += (double)g;
+        }
+        const double tot = block_sum_d(s, red);
+        if (threadIdx.x == 0 && a.gbias) a.gbias[c] = (float)tot;
+        return;
+    }
+    const float cs = bn_lip_scale(a.gamma, a.C, red);
+    const float m32 = a.mean[c], is32 = a.invstd[c];
+    double sg = 0.0, sgx = 0.0;
+    for (int i = threadIdx.x; i < a.P; i += blockDim.x) {
+        const float g = act_bwd(gy[i], y[i], a.act);
+        const float xh = (z[i] - m32) * is32;
+        sg += (double)g;
+        sgx += (double)g * (double)xh;
+    }
+    sg = block_sum_d(sg, red);
+    sgx = block_sum_d(sgx, red);
+    const float gm = a.gamma[c] / cs;
+    const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
+    const float k = gm * is32;
+    double sb = 0.0;
+    for (int i = threadIdx.x; i < a.P; i += blockDim.x) {
+        const float g = act_bwd(gy[i], y[i], a.act);
+        const float xh = (z[i] - m32) * is32;
+        const float d = k * (g - mg - xh * mgx);
+        gz[i] = d;
+        sb += (double)d;
+    }
+    sb = block_sum_d(sb, red);
+    if (threadIdx.x == 0) {
+        a.ggamma[c] = (float)sgx / cs;
+        a.gbeta[c] = (float)sg / cs;
+        if (a.gbias) a.gbias[c] = (float)sb;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// sigma_max of every conv weight W (rows x cols), batched: one conv per blockIdx.y.
+// Gram on the smaller side (m = min(rows, cols) <= 128) in fp64, exact products.
+// ------------------------------------------------------------------------------------------
+constexpr int kSnMaxDim = 128;
+
+__global__ __launch_bounds__(256) void k_sn_gram(const SnConv *convs, double *gram) {
+    const SnConv cv = convs[blockIdx.y];
+    const bool rowside = cv.rows <= cv.cols;    // G = W W^T (rows) or W^T W (cols)
+    const int m = rowside ? cv.rows : cv.cols;
+    const int inner = rowside ? cv.cols : cv.rows;
+    const int tiles = (m + 31) / 32;
+    if ((int)blockIdx.x >= tiles * tiles) return;
+    const int ti = blockIdx.x / tiles, tj = blockIdx.x % tiles;
+    __shared__ float Si[32][33], Sj[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 8 rows of 32
+    double acc[4] = {0, 0, 0, 0};
+    double *G = gram + (int64_t)blockIdx.y * kSnMaxDim * kSnMaxDim;
+    for (int k0 = 0; k0 < inner; k0 += 32) {
+        // Si[r][kk] = V(ti*32 + r, k0 + kk) where V(i, k) = rowside ? W[i][k] : W[k][i]
+        for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+            const int r = e >> 5, kk = e & 31;
+            const int ii = ti * 32 + r, jj = tj * 32 + r, k = k0 + kk;
+            float vi = 0.f, vj = 0.f;
+            if (k < inner) {
+                if (rowside) {
+                    if (ii < m) vi = cv.W[(int64_t)ii * cv.cols + k];
+                    if (jj < m) vj = cv.W[(int64_t)jj * cv.cols + k];
+                } else {
+                    if (ii < m) vi = cv.W[(int64_t)k * cv.cols + ii];
+                    if (jj < m) vj = cv.W[(int64_t)k * cv.cols + jj];
+                }
+            }
+            Si[r][kk] = vi;
+            Sj[r][kk] = vj;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int kk = 0; kk < 32; ++kk) {
+            const double b = (double)Sj[tx][kk];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = __fma_rn((double)Si[ty + 8 * q][kk], b, acc[q]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i = ti * 32 + ty + 8 * q, j = tj * 32 + tx;
+        if (i < m && j < m) G[i * kSnMaxDim + j] = acc[q];
+    }
+}
+
+__device__ int sturm_gt(const double *al, const double *be2, int k, double x) {
+    int neg = 0;
+    double d = 1.0;
+    for (int i = 0; i < k; ++i) {
+        d = (al[i] - x) - (i > 0 ? be2[i - 1] / d : 0.0);
+        if (d == 0.0) d = -1e-300;
+        neg += d < 0.0;
+    }
+    return k - neg;
+}
+
+// One workgroup (256 threads) per conv: Lanczos (no reorthogonalisation: the extreme Ritz value
+// converges regardless, Paige) run for m steps with the Gram in registers (thread t holds half a
+// row, 64 doubles), then a 256-point multisection of the tridiagonal for lambda_max.
+// sigma32 = float(sqrt(lambda_max)); scale = max(1, sigma32 / ln_lambda) (float32, as torch).
+__global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const double *gram, float *sigma,
+                                                  float *scale, float ln_lambda) {
+    const SnConv cv = convs[blockIdx.x];
+    const int m = cv.rows <= cv.cols ? cv.rows : cv.cols;
+    const double *G = gram + (int64_t)blockIdx.x * kSnMaxDim * kSnMaxDim;
+    __shared__ double q[kSnMaxDim], al[kSnMaxDim], be2[kSnMaxDim], red[8];
+    __shared__ double lo_s, hi_s;
+    __shared__ int best_s;
+    const int t = threadIdx.x, row = t >> 1, half = t & 1;
+    double g[64];
+#pragma unroll
+    for (int c = 0; c < 64; ++c) {
+        const int col = half * 64 + c;
+        g[c] = (row < m && col < m) ? G[row * kSnMaxDim + col] : 0.0;
+    }
+    // q0 = normalised deterministic start vector
+    double qr = 0.0, qprev = 0.0, wr;
+    if (row < m) qr = 1.0 + 0.5 * sin(0.7 * (double)row + 0.3);
+    {
+        const double nn = block_sum_d(half == 0 ? qr * qr : 0.0, red);
+        qr = qr / sqrt(nn);
+    }
+    if (half == 0) q[row] = qr;
+    __syncthreads();
+    double beta = 0.0;
+    int k = 0;
+    for (; k < m; ++k) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < 64; ++c) s = __fma_rn(g[c], q[half * 64 + c], s);
+        s += __shfl_xor(s, 1, 64);
+        wr = s;                                   // (G q)_row, both halves
+        const double a = block_sum_d(half == 0 ? qr * wr : 0.0, red);
+        wr = wr - a * qr - beta * qprev;
+        const double b2 = block_sum_d(half == 0 ? wr * wr : 0.0, red);
+        if (t == 0) { al[k] = a; be2[k] = b2; }
+        const double b = sqrt(b2);
+        if (!(b > 1e-14 * fabs(a)) || k + 1 == m) { ++k; break; }
+        qprev = qr;
+        qr = wr / b;
+        beta = b;
+        __syncthreads();                          // all reads of q done
+        if (half == 0) q[row] = qr;
+        __syncthreads();
+    }
+    __syncthreads();
+    // Gershgorin interval of T_k, then multisection
+    if (t == 0) {
+        double lo = 1e300, hi = -1e300;
+        for (int i = 0; i < k; ++i) {
+            const double r = (i > 0 ? sqrt(be2[i - 1]) : 0.0) + (i + 1 < k ? sqrt(be2[i]) : 0.0);
+            lo = fmin(lo, al[i] - r);
+            hi = fmax(hi, al[i] + r);
+        }
+        lo_s = fmax(lo, 0.0);
+        hi_s = hi;
+    }
+    __syncthreads();
+    for (int round = 0; round < 10; ++round) {
+        const double lo = lo_s, hi = hi_s;
+        if (!(hi - lo > 0.0)) break;
+        const double x = lo + (hi - lo) * (double)(t + 1) / 257.0;
+        if (t == 0) best_s = -1;
+        __syncthreads();
+        if (x > lo && x < hi && sturm_gt(al, be2, k, x) >= 1) atomicMax(&best_s, t);
+        __syncthreads();
+        if (t == 0) {
+            const int bt = best_s;
+            const double nlo = bt >= 0 ? lo + (hi - lo) * (double)(bt + 1) / 257.0 : lo;
+            const double nhi = bt + 1 <= 255 ? lo + (hi - lo) * (double)(bt + 2) / 257.0 : hi;
+            lo_s = nlo;
+            hi_s = fmax(nlo, nhi);
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const double lmax = m > 0 ? 0.5 * (lo_s + hi_s) : 0.0;
+        const float s32 = (float)sqrt(fmax(lmax, 0.0));
+        sigma[blockIdx.x] = s32;
+        scale[blockIdx.x] = fmaxf(1.0f, s32 / ln_lambda);
+    }
+}
+
+// Wn = W_bar / scale  (all convs; blockIdx.y = conv)
+__global__ void k_sn_apply(const SnConv *convs, const float *scale) {
+    const SnConv cv = convs[blockIdx.y];
+    const int64_t n = (int64_t)cv.rows * cv.cols;
+    const float s = scale[blockIdx.y];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        cv.Wn[i] = cv.W[i] / s;
+}
+
+// ------------------------------------------------------------------------------------------
+// Loss: mse(target*mask, out*mask) over C*P (main_LRS_PnP_DIP_1-LiP.py:234); gout = dL/dout.
+// mask is [P] (broadcast over channels, mask_bkg (1,1,H,W)) or null.
+// ------------------------------------------------------------------------------------------
+__global__ void k_masked_mse(const float *__restrict__ out, const float *__restrict__ target,
+                             const float *__restrict__ mask, int C, int64_t P, float *__restrict__ gout,
+                             double *loss_acc) {
+    __shared__ double red[4];
+    const int64_t N = (int64_t)C * P;
+    const float norm = (float)(2.0 / (double)N);
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        const float mk = mask ? mask[i % P] : 1.0f;
+        const float a = target[i] * mk, b = out[i] * mk;
+        const float d = a - b;
+        s += (double)d * (double)d;
+        if (gout) gout[i] = (-(norm * d)) * mk;
+    }
+    s = block_sum_d(s, red);
+    if (threadIdx.x == 0) atomicAdd(loss_acc, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// Adam (torch.optim.Adam defaults: no weight decay, no amsgrad), flat parameter buffer.
+// step is a device counter so a captured step replays correctly.
+// ------------------------------------------------------------------------------------------
+__global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
+                       float *__restrict__ v, int64_t n, const int *step, float lr, float b1, float b2,
+                       float eps) {
+    const int t = *step;
+    const double bc1 = 1.0 - pow((double)b1, (double)t);
+    const double bc2 = 1.0 - pow((double)b2, (double)t);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = g[i];
+        const float mi = m[i] + (1.0f - b1) * (gi - m[i]);          // exp_avg.lerp_(grad, 1-b1)
+        const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;         // mul_(b2).addcmul_(g, g, 1-b2)
+        m[i] = mi;
+        v[i] = vi;
+        const float den = sqrtf(vi) / bc2s + eps;
+        p[i] = p[i] - step_size * (mi / den);
+    }
+}
+
+__global__ void k_counter_inc(int *c) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *c += 1;
+}
+
+// ------------------------------------------------------------------------------------------
+// Early stopping (main_LRS_PnP_DIP_1-LiP.py:71-99, 244-264), on device.
+// ring: [size][N] of the last outputs; slot = (count-1) % size holds the newest.
+// var = mean_i sum_p (ave_p - img_i,p)^2 / N  (myMetric, :102-103), accumulated in fp64.
+// ------------------------------------------------------------------------------------------
+__global__ void k_es_push(const float *__restrict__ out, int64_t N, float *__restrict__ ring, lrs_es_state *st) {
+    const int slot = st->count % st->size;
+    float *dst = ring + (int64_t)slot * N;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = out[i];
+}
+
+__global__ void k_es_var(const float *__restrict__ ring, int64_t N, lrs_es_state *st) {
+    __shared__ double red[4];
+    if (st->count + 1 < st->size) return;   // count is incremented by k_es_decide
+    const int S = st->size;
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        double ave = 0.0;
+        for (int j = 0; j < S; ++j) ave += (double)ring[(int64_t)j * N + i];
+        ave /= S;
+        for (int j = 0; j < S; ++j) {
+            const double d = ave - (double)ring[(int64_t)j * N + i];
+            s += d * d;
+        }
+    }
+    s = block_sum_d(s, red);
+    if (threadIdx.x == 0) atomicAdd(&st->var_acc, s);
+}
+
+__global__ void k_es_decide(int64_t N, lrs_es_state *st) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int epoch = st->count;           // iteration index i of the reference loop
+    st->count += 1;
+    if (st->count >= st->size && !st->stop) {
+        const double var = st->var_acc / (double)N / (double)st->size;
+        st->last_var = var;
+        if (var < st->best) {
+            st->best = var;
+            st->best_epoch = epoch;
+            st->wait = 0;
+        } else {
+            st->wait += 1;
+            if (st->wait >= st->patience) {
+                st->stop = 1;
+                st->stop_epoch = epoch;
+            }
+        }
+    }
+    st->var_acc = 0.0;
+}
+
+}  // namespace lrs

@@ -59,6 +59,38 @@ def _declare(L):
         "lrs_diag_svt_state": (i32, [vp, i64, i64, vp]),
         "lrs_admm_update_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, i64, vp, vp,
                                       vp, vp, f32, f32, f32, vp, vp, vp]),
+        # DIP low-rank prox
+        "lrs_conv2d_out_size": (i32, [i32, i32, i32, i32, i32, i32, c.POINTER(c.c_int), c.POINTER(c.c_int)]),
+        "lrs_conv2d_col_size": (i64, [i32, i32, i32, i32, i32, i32, i32]),
+        "lrs_conv2d_workspace": (sz, [i32, i32, i32, i32, i32, i32, i32, i32]),
+        "lrs_conv2d_fwd_f32": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, sz, vp]),
+        "lrs_conv2d_bwd_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, sz,
+                                     vp]),
+        "lrs_bn_act_fwd_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, f32, f32, vp]),
+        "lrs_bn_act_bwd_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, vp]),
+        "lrs_sigma_max_workspace": (sz, [i32]),
+        "lrs_sigma_max_f32": (i32, [c.POINTER(vp), c.POINTER(vp), c.POINTER(c.c_int), c.POINTER(c.c_int), i32,
+                                    f32, vp, vp, vp, sz, vp]),
+        "lrs_adam_f32": (i32, [vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, vp]),
+        "lrs_masked_mse_f32": (i32, [vp, vp, vp, i32, i64, vp, vp, vp]),
+        "lrs_es_init": (i32, [vp, i32, i32, vp]),
+        "lrs_es_update_f32": (i32, [vp, i64, vp, vp, vp]),
+        "lrs_dipnet_create": (i32, [vp, i32, i32, i32, c.POINTER(vp)]),
+        "lrs_dipnet_destroy": (None, [vp]),
+        "lrs_dipnet_num_params": (i64, [vp]),
+        "lrs_dipnet_num_bnstats": (i64, [vp]),
+        "lrs_dipnet_workspace": (sz, [vp]),
+        "lrs_dipnet_param_offsets": (i32, [vp, i32, c.POINTER(i64), c.POINTER(i64), c.POINTER(i64),
+                                           c.POINTER(i64)]),
+        "lrs_dipnet_out_shape": (i32, [vp, c.POINTER(c.c_int), c.POINTER(c.c_int), c.POINTER(c.c_int)]),
+        "lrs_dipnet_bind": (i32, [vp, vp, vp, vp, vp, vp, vp, sz]),
+        "lrs_dipnet_init_params": (i32, [vp, c.c_uint64, vp]),
+        "lrs_dipnet_reset_optimizer": (i32, [vp, vp]),
+        "lrs_dipnet_forward": (i32, [vp, vp, vp]),
+        "lrs_dipnet_output": (c.c_size_t, [vp]),
+        "lrs_dipnet_grads": (c.c_size_t, [vp]),
+        "lrs_dipnet_train_steps": (i32, [vp, vp, vp, vp, f32, f32, f32, f32, vp, vp, i32, i32, vp]),
+        "lrs_dipnet_last_loss": (i32, [vp, c.POINTER(f64), vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,97 @@
+"""CPU: the torch restatement of the 1-Lip U-Net (tests/dip_ref.py) against the reference's own
+my_Lipschitz_Unet outputs (tests/golden/dip_golden.npz), and the engine's host-side layout."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+import dip_ref  # noqa: E402
+from gen_dip_golden import flat_params, problem  # noqa: E402
+from lrspnp.dip import ConvUnit, lipschitz_unet_units, unet_size_ok  # noqa: E402
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def gold(golden):
+    return golden("dip_golden.npz")
+
+
+def test_restatement_matches_reference_unet(gold):
+    torch.manual_seed(0)
+    units = lipschitz_unet_units(128, 128, 128)
+    flat = torch.from_numpy(flat_params(units, int(gold["seed"])))
+    x, target, mask = (torch.from_numpy(a) for a in problem(int(gold["seed"])))
+    # sigma_max of every conv (SpectralNorm._update_u_v)
+    offs, _ = dip_ref.param_offsets(units)
+    sig = [float(dip_ref.sigma_scale(dip_ref.views(flat, units, i, offs)[0])[0]) for i in range(len(units))]
+    np.testing.assert_allclose(sig, gold["sigma"], rtol=2e-6)
+    tr = dip_ref.RefTrainer(units, flat, lr=0.1)
+    sub = int(gold["sub"])
+    for it in range(int(gold["steps"])):
+        out, loss, g = tr.step(x, target, mask)
+        if it > 0:
+            # Adam's first steps are sign-like (lr * g/|g|), so rounding-level gradient differences
+            # flip whole +-lr moves: the reference itself, run with 1 vs 3 CPU threads, differs by
+            # 8-10 % in the output after one step and 65-70 % after two.  Later steps are only
+            # held to the loss band that self-spread allows.
+            assert abs(loss - gold["loss"][it]) <= 0.2 * gold["loss"][it], (it, loss, gold["loss"][it])
+            continue
+        assert abs(loss - gold["loss"][0]) <= 1e-6 * gold["loss"][0], (loss, gold["loss"][0])
+        assert rel(out.numpy().reshape(-1)[::sub], gold["out_sub"][0]) < 1e-5
+        if it == 0:
+            gn = []
+            for i in range(len(units)):
+                W, b, gm, be = dip_ref.views(g, units, i, offs)
+                gn += [float(W.norm()), float(b.norm()), float(gm.norm()) if gm is not None else 0.0,
+                       float(be.norm()) if be is not None else 0.0]
+            gn, ref = np.array(gn), gold["grad_norms"]
+            big = ref > 1e-4 * ref.max()            # pre-BN bias grads are rounding noise
+            np.testing.assert_allclose(gn[big], ref[big], rtol=1e-4)
+
+
+def test_engine_layout_matches_restatement():
+    from lrspnp import _lib
+    L = _lib.lib()
+    units = lipschitz_unet_units(128, 198, 128)
+    arr = (ConvUnit * len(units))(*units)
+    h = ctypes.c_void_p()
+    assert L.lrs_dipnet_create(arr, len(units), 196, 196, ctypes.byref(h)) == 0
+    try:
+        offs, n = dip_ref.param_offsets(units)
+        assert L.lrs_dipnet_num_params(h) == n
+        for i, o in enumerate(offs):
+            got = [ctypes.c_int64() for _ in range(4)]
+            assert L.lrs_dipnet_param_offsets(h, i, *[ctypes.byref(x) for x in got]) == 0
+            assert tuple(x.value for x in got) == o
+        c, ho, wo = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        L.lrs_dipnet_out_shape(h, ctypes.byref(c), ctypes.byref(ho), ctypes.byref(wo))
+        assert (c.value, ho.value, wo.value) == (198, 196, 196)
+        assert L.lrs_dipnet_workspace(h) > 0
+    finally:
+        L.lrs_dipnet_destroy(h)
+
+
+def test_unet_sizes():
+    # my_Lipschitz_Unet returns to the input size only for some H (36 native, 196 for 200x200 cubes)
+    assert unet_size_ok(36, 36) and unet_size_ok(196, 196)
+    assert not unet_size_ok(200, 200)
+
+
+def test_early_stop_restatement_logic():
+    es = dip_ref.EarlyStopRef(size=3, patience=2)
+    seq = [np.full(4, v, np.float32) for v in (0, 1, 0, 1, 1, 1, 1, 1)]
+    stops = [es.update(s, i) for i, s in enumerate(seq)]
+    # variance decreases once the ring is flat: 2/9 (i=2), 2/9 (i=3, not <), 2/9 -> wait 2 -> stop at 4? no:
+    assert es.vars[0] > 0
+    assert stops[-1] and es.stop_epoch is not None and es.stop_epoch >= 3

@@ -1,0 +1,296 @@
+"""GPU: DIP low-rank prox kernels (lrs_conv2d_*, lrs_bn_act_*, lrs_sigma_max_f32, lrs_adam_f32,
+lrs_masked_mse_f32, lrs_es_*) and the lrs_dipnet engine, against plain PyTorch fp32 on the CPU
+(tests/dip_ref.py, itself pinned to the reference's my_Lipschitz_Unet by tests/test_dip_ref.py).
+
+Tolerances (relative L2 unless noted): single layers 1e-5 (fwd) / 2e-5 (bwd); sigma_max 2e-6
+vs fp64 SVD; whole-net forward 1e-5, loss 1e-6, step-0 gradients 1e-4; Adam 1e-6.
+Multi-step trajectories are chaotic (see test_dip_ref.py) and are compared step by step from
+identical states instead.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.nn.functional as F  # noqa: E402
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+import dip_ref  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double().cpu(); b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-300))
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lrspnp import _lib
+    return _lib.device_lib()
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def S():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+CONV_CASES = [
+    # cin, cout, H, W, k, stride, pad, pad_mode, up
+    (128, 128, 36, 36, 3, 2, 1, 1, 0),      # d_1 first conv
+    (128, 128, 18, 18, 3, 1, 1, 1, 0),
+    (128, 128, 3, 3, 3, 1, 1, 1, 0),        # bottleneck: reflection on a 3x3 map (3 mirrors)
+    (128, 128, 3, 3, 2, 1, 0, 1, 1),        # up_1: upsample + 2x2
+    (128, 128, 9, 9, 3, 1, 1, 1, 1),        # up_3
+    (128, 198, 36, 36, 1, 1, 0, 1, 0),      # last 1x1 (plain)
+    (7, 5, 11, 6, 3, 2, 1, 0, 0),           # zero padding, odd sizes
+    (5, 9, 5, 7, 3, 1, 1, 1, 1),
+]
+
+
+def torch_conv(x, w, b, k, stride, pad, pad_mode, up):
+    h = x[None]
+    if up:
+        h = F.interpolate(h, scale_factor=2, mode="nearest")
+    if pad:
+        h = F.pad(h, (pad,) * 4, mode="reflect" if pad_mode == 1 else "constant")
+    return F.conv2d(h, w, b, stride=stride)[0]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(L, case):
+    cin, cout, H, W, k, stride, pad, pm, up = case
+    g = torch.Generator().manual_seed(hash(case) & 0xffff)
+    x = torch.randn(cin, H, W, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / np.sqrt(cin * k * k)
+    b = torch.randn(cout, generator=g) * 0.1
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yr = torch_conv(xr, wr, b, k, stride, pad, pm, up)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy)
+    Ho, Wo = yr.shape[1:]
+    xd, wd, bd, gyd = (t.cuda().contiguous() for t in (x, w, b, gy))
+    ncol = L.lrs_conv2d_col_size(cin, H, W, k, stride, pad, up)
+    col = torch.empty(max(ncol, 1), device="cuda")
+    nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, stride, pad, up)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    y = torch.empty(cout, Ho, Wo, device="cuda")
+    assert L.lrs_conv2d_fwd_f32(P(xd), cin, H, W, P(wd), P(bd), cout, k, stride, pad, pm, up,
+                                P(col) if ncol else None, P(y), P(ws), nws, S()) == 0
+    assert rel(y, yr.detach()) < 1e-5
+    div = torch.tensor([1.7], device="cuda")
+    gw = torch.empty_like(wd)
+    gx = torch.empty_like(xd)
+    assert L.lrs_conv2d_bwd_f32(P(gyd), P(col) if ncol else P(xd), P(wd), P(div), cin, H, W, cout, k, stride,
+                                pad, pm, up, P(gx), P(gw), P(ws), nws, S()) == 0
+    torch.cuda.synchronize()
+    assert rel(gw, wr.grad / 1.7) < 2e-5
+    assert rel(gx, xr.grad) < 2e-5
+
+
+@pytest.mark.parametrize("bn,act,C,HW", [(1, 1, 128, 36 * 36), (1, 1, 64, 9), (0, 1, 198, 1296), (1, 2, 16, 100)])
+def test_bn_act(L, bn, act, C, HW):
+    g = torch.Generator().manual_seed(C + HW)
+    z = torch.randn(C, HW, generator=g) * 2 + 0.5
+    gamma = 1 + 0.5 * torch.rand(C, generator=g)       # max > 1: the Lipschitz rescale is active
+    beta = 0.2 * torch.randn(C, generator=g)
+    gy = torch.randn(C, HW, generator=g)
+    zr, gr, br = z.clone().requires_grad_(True), gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    h = zr[None, :, :, None]
+    if bn:
+        c = max(float(gamma.abs().max()), 1.0)
+        h = F.batch_norm(h, None, None, gr / c, br / c, training=True, eps=1e-5)
+    yr = (F.leaky_relu(h, 0.2) if act == 1 else torch.sigmoid(h))[0, :, :, 0]
+    yr.backward(gy)
+    zd, gmd, btd, gyd = (t.cuda().contiguous() for t in (z, gamma, beta, gy))
+    y = torch.empty_like(zd)
+    mean, istd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    assert L.lrs_bn_act_fwd_f32(P(zd), P(y), P(gmd) if bn else None, P(btd) if bn else None, P(mean), P(istd),
+                                P(rm) if bn else None, P(rv) if bn else None, C, HW, act, ctypes.c_float(1e-5),
+                                ctypes.c_float(0.1), S()) == 0
+    assert rel(y, yr.detach()) < 1e-5
+    gz = torch.empty_like(zd)
+    gg, gb, gbias = torch.empty(C, device="cuda"), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    assert L.lrs_bn_act_bwd_f32(P(gyd), P(y), P(zd), P(gmd) if bn else None, P(mean), P(istd), P(gz),
+                                P(gg) if bn else None, P(gb) if bn else None, P(gbias), C, HW, act, S()) == 0
+    torch.cuda.synchronize()
+    assert rel(gz, zr.grad) < 2e-5
+    assert rel(gbias, zr.grad.sum(1)) < 1e-3 or float(zr.grad.sum(1).abs().max()) < 1e-4
+    if bn:
+        assert rel(gg, gr.grad) < 2e-5 and rel(gb, br.grad) < 2e-5
+        var = z.double().var(1, unbiased=True)
+        assert rel(rv, 0.9 + 0.1 * var) < 1e-5 and rel(rm, 0.1 * z.double().mean(1)) < 1e-5
+
+
+def test_sigma_max(L):
+    from lrspnp.dip import sigma_max
+    g = torch.Generator().manual_seed(5)
+    mats = [torch.randn(128, 1152, generator=g) * 0.04, torch.randn(128, 512, generator=g) * 0.06,
+            torch.randn(128, 128, generator=g) * 0.1, torch.randn(198, 128, generator=g) * 0.1,
+            torch.randn(7, 3, generator=g),
+            (torch.randn(128, 4, generator=g) @ torch.randn(4, 300, generator=g)) * 0.01,   # rank 4
+            torch.full((64, 64), 0.01)]                                                    # rank 1
+    sig, sc = sigma_max([m.cuda() for m in mats])
+    ref = torch.tensor([float(torch.linalg.svdvals(m.double())[0]) for m in mats])
+    np.testing.assert_allclose(sig.cpu().double().numpy(), ref.numpy(), rtol=2e-6)
+    np.testing.assert_allclose(sc.cpu().numpy(), np.maximum(1.0, sig.cpu().numpy()))
+
+
+def test_adam_matches_torch(L):
+    g = torch.Generator().manual_seed(2)
+    p0 = torch.randn(10007, generator=g)
+    p = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([p], lr=0.1)
+    pd, md, vd = p0.cuda(), torch.zeros(10007, device="cuda"), torch.zeros(10007, device="cuda")
+    step = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for it in range(4):
+        gr = torch.randn(10007, generator=g) * (10.0 ** -it)
+        p.grad = gr.clone()
+        opt.step()
+        step += 1
+        assert L.lrs_adam_f32(P(pd), P(gr.cuda()), P(md), P(vd), 10007, P(step), ctypes.c_float(0.1),
+                              ctypes.c_float(0.9), ctypes.c_float(0.999), ctypes.c_float(1e-8), S()) == 0
+        torch.cuda.synchronize()
+        assert rel(pd, p.detach()) < 1e-6
+
+
+def test_masked_mse(L):
+    g = torch.Generator().manual_seed(3)
+    out, tgt = torch.randn(128, 36, 36, generator=g), torch.randn(128, 36, 36, generator=g)
+    mask = (torch.rand(36, 36, generator=g) > 0.3).float()
+    o = out.clone().requires_grad_(True)
+    loss = F.mse_loss(tgt * mask, o * mask)
+    loss.backward()
+    acc = torch.zeros(1, dtype=torch.float64, device="cuda")
+    gout = torch.empty(128, 36, 36, device="cuda")
+    assert L.lrs_masked_mse_f32(P(out.cuda()), P(tgt.cuda()), P(mask.cuda()), 128, 1296, P(gout), P(acc), S()) == 0
+    torch.cuda.synchronize()
+    assert abs(float(acc) / out.numel() - float(loss.detach())) < 1e-6 * float(loss.detach())
+    assert rel(gout, o.grad) < 1e-6
+
+
+def test_early_stop_device_vs_reference_logic(L):
+    from lrspnp.dip import EarlyStopper
+    g = torch.Generator().manual_seed(4)
+    N, size, patience = 500, 5, 4
+    es = EarlyStopper(N, size, patience)
+    ref = dip_ref.EarlyStopRef(size, patience)
+    base = torch.randn(N, generator=g)
+    stop_ref = None
+    for i in range(40):
+        scale = 1.0 / (1 + i) if i < 12 else 0.05 * (1 + (i % 3))   # variance falls, then plateaus
+        img = base + scale * torch.randn(N, generator=g)
+        if ref.update(img.numpy(), i) and stop_ref is None:
+            stop_ref = ref.stop_epoch
+        assert L.lrs_es_update_f32(P(img.cuda()), N, P(es.ring), P(es.state), None) == 0
+    st = es.read()
+    assert stop_ref is not None and st.stop == 1 and st.stop_epoch == stop_ref
+    np.testing.assert_allclose(st.best, min(ref.vars), rtol=1e-9)
+
+
+# ---- whole network -----------------------------------------------------------------------------
+def _problem(gold_seed=1234, units=None):
+    from gen_dip_golden import flat_params, problem
+    from lrspnp.dip import lipschitz_unet_units
+    units = units or lipschitz_unet_units(128, 128, 128)
+    flat = torch.from_numpy(flat_params(units, gold_seed))
+    x, t, m = (torch.from_numpy(a) for a in problem(gold_seed))
+    return units, flat, x, t, m
+
+
+def _engine(units, flat, H=36, W=36):
+    from lrspnp.dip import DipNet
+    net = DipNet(units, H, W)
+    net.params.copy_(flat.cuda())
+    net.reset_optimizer()
+    return net
+
+
+def test_unet_forward_and_first_step_vs_reference(L, golden):
+    gold = golden("dip_golden.npz")
+    units, flat, x, t, m = _problem(int(gold["seed"]))
+    net = _engine(units, flat)
+    out = net.forward(x.cuda()).cpu()
+    sub = int(gold["sub"])
+    assert rel(out.reshape(-1)[::sub], torch.from_numpy(gold["out_sub"][0])) < 1e-5     # the reference module
+    ref = dip_ref.forward(flat, units, x)
+    assert rel(out, ref) < 1e-5
+    # one training step from the same state: loss, gradients, the Adam update.  Gradients are
+    # compared with the restatement in fp64 (the engine is ~2e-5 from it; fp32 CPU torch on the GPU
+    # hosts measured 1.8e-3 from fp64 at the first layer, so fp32 CPU is not a tight reference).
+    tr = dip_ref.RefTrainer(units, flat)
+    out_r, loss_r, _ = tr.step(x, t, m.reshape(-1))
+    p64 = flat.double().clone().requires_grad_(True)
+    dip_ref.loss_fn(dip_ref.forward(p64, units, x.double()), t.double(), m.reshape(-1).double()).backward()
+    g_r = p64.grad
+    net.train_steps(x.cuda(), t.cuda(), m.reshape(-1).cuda(), 1, use_graph=False)
+    torch.cuda.synchronize()
+    assert abs(net.last_loss() - loss_r) < 1e-6 * loss_r
+    assert abs(net.last_loss() - gold["loss"][0]) < 1e-6 * gold["loss"][0]
+    gd = net.grads.cpu()
+    offs, _ = dip_ref.param_offsets(units)
+    for i in range(len(units)):
+        Wg, bg, gg, beg = dip_ref.views(gd, units, i, offs)
+        Wr, br, gr, ber = dip_ref.views(g_r, units, i, offs)
+        assert rel(Wg, Wr) < 1e-4, i
+        if gg is not None:
+            assert rel(gg, gr) < 1e-4 and rel(beg, ber) < 1e-4, i
+        else:
+            assert rel(bg, br) < 1e-4, i          # biases before a BN are rounding noise; skip those
+    # first Adam move = -lr * g / (|g| + eps): identical except where a rounding-level gradient flips sign
+    expect = flat.double() - 0.1 * g_r / (g_r.abs() + 1e-8)
+    dp = (net.params.cpu().double() - expect).abs()
+    keep = torch.ones_like(dp, dtype=torch.bool)
+    for i, u in enumerate(units):                 # biases before a BN: zero gradient in exact arithmetic
+        if u.bn:
+            keep[offs[i][1]:offs[i][1] + u.cout] = False
+    assert float((dp[keep] > 1e-4).float().mean()) < 1e-3
+
+
+def test_unet_graph_replay_equals_eager(L):
+    units, flat, x, t, m = _problem()
+    xd, td, md = x.cuda(), t.cuda(), m.reshape(-1).cuda()
+    a = _engine(units, flat)
+    a.train_steps(xd, td, md, 4, use_graph=False)
+    b = _engine(units, flat)
+    b.train_steps(xd, td, md, 1, use_graph=True)      # capture + 1 replay
+    b.train_steps(xd, td, md, 3, use_graph=True)      # replays
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.exp_avg_sq, b.exp_avg_sq)
+    assert torch.equal(a.output(), b.output())
+
+
+def test_unet_generalised_bands_196(L):
+    """in = out = 198 bands, hidden 128, 196 x 196 (SURVEY.md §8 a8 generalised config)."""
+    from lrspnp.dip import lipschitz_unet_units
+    units = lipschitz_unet_units(198, 198, 128)
+    g = torch.Generator().manual_seed(9)
+    from gen_dip_golden import flat_params
+    flat = torch.from_numpy(flat_params(units, 77))
+    x = torch.rand(198, 196, 196, generator=g)
+    net = _engine(units, flat, 196, 196)
+    out = net.forward(x.cuda()).cpu()
+    assert out.shape == (198, 196, 196)
+    assert rel(out, dip_ref.forward(flat, units, x)) < 1e-5
+
+
+def test_lipschitz_dip_run_early_stop(L):
+    from lrspnp.dip import DipConfig, LipschitzDip
+    units, flat, x, t, m = _problem()
+    dip = LipschitzDip(128, 36, 36, DipConfig(num_iter=400, poll_every=10))
+    out = dip.run(t.cuda(), x.cuda(), m.reshape(-1).cuda(), seed=3)
+    assert out.shape == (128, 36, 36) and torch.isfinite(out).all()
+    assert dip.last_stop_epoch is None or dip.last_stop_epoch >= 89   # >= 30 + 60 - 1 steps
+    out2 = dip.run(t.cuda(), x.cuda(), m.reshape(-1).cuda(), seed=3, num_iter=5, early_stop=False)
+    assert torch.isfinite(out2).all()
