@@ -184,6 +184,12 @@ int lrs_adam_f32(float *p, const float *g, float *m, float *v, int64_t n, const 
 int lrs_masked_mse_f32(const float *out, const float *target, const float *mask, int C, int64_t P,
                        float *gout, double *loss_acc, void *stream);
 
+/* Layout transforms between the unfolded matrix X[p = i + H j][b] and the DIP image img[b][i][j]
+ * (…1-LiP.py:404 DIP_input = X + (1/mu_2) lambda_2 as (1,B,H,W); :411 U back to (P,B)). */
+int lrs_unfolded_to_image_f32(const float *X, const float *L, float c, int64_t H, int64_t W, int64_t B,
+                              float *img, void *stream);
+int lrs_image_to_unfolded_f32(const float *img, int64_t H, int64_t W, int64_t B, float *X, void *stream);
+
 /* Early stopping state (device memory).  lrs_es_init fills it; every lrs_es_update_f32 pushes one
  * output into the ring [size][N] and, once full, applies the variance test. */
 typedef struct {

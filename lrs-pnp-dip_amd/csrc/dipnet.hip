@@ -210,6 +210,30 @@ __global__ void k_fill(float *p, int64_t n, float v) {
         p[i] = v;
 }
 
+// img[b][i][j] = X[(i + H j) B + b] + c * L[...]   (…1-LiP.py:404; L nullable)
+__global__ void k_unfolded_to_image(const float *__restrict__ X, const float *__restrict__ L, float c, int64_t H,
+                                    int64_t W, int64_t B, float *__restrict__ img) {
+    const int64_t n = H * W * B;
+    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = o % W, i = (o / W) % H, b = o / (W * H);
+        const int64_t src = (i + H * j) * B + b;
+        float v = X[src];
+        if (L) v = v + c * L[src];
+        img[o] = v;
+    }
+}
+
+// X[(i + H j) B + b] = img[b][i][j]   (…1-LiP.py:411)
+__global__ void k_image_to_unfolded(const float *__restrict__ img, int64_t H, int64_t W, int64_t B,
+                                    float *__restrict__ X) {
+    const int64_t n = H * W * B;
+    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = o % B, p = o / B;
+        const int64_t i = p % H, j = p / H;
+        X[o] = img[(b * H + i) * W + j];
+    }
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -325,6 +349,23 @@ extern "C" int lrs_masked_mse_f32(const float *out, const float *target, const f
     if (!out || !target || !loss_acc || C <= 0 || P <= 0) return LRS_E_INVALID;
     hipLaunchKernelGGL(k_masked_mse, dim3(ew_blocks((int64_t)C * P, 2048)), dim3(kEw), 0, (hipStream_t)stream, out,
                        target, mask, C, P, gout, loss_acc);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+extern "C" int lrs_unfolded_to_image_f32(const float *X, const float *L, float c, int64_t H, int64_t W, int64_t B,
+                                         float *img, void *stream) {
+    if (!X || !img || H <= 0 || W <= 0 || B <= 0) return LRS_E_INVALID;
+    hipLaunchKernelGGL(k_unfolded_to_image, dim3(ew_blocks(H * W * B, 8192)), dim3(kEw), 0, (hipStream_t)stream, X,
+                       L, c, H, W, B, img);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+extern "C" int lrs_image_to_unfolded_f32(const float *img, int64_t H, int64_t W, int64_t B, float *X, void *stream) {
+    if (!X || !img || H <= 0 || W <= 0 || B <= 0) return LRS_E_INVALID;
+    hipLaunchKernelGGL(k_image_to_unfolded, dim3(ew_blocks(H * W * B, 8192)), dim3(kEw), 0, (hipStream_t)stream,
+                       img, H, W, B, X);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }

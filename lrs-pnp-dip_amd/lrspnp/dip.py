@@ -131,11 +131,9 @@ class DipNet:
 
     # ---- parameters ---------------------------------------------------------------------------
     def init_params(self, seed: int):
-        import torch
-        torch.cuda.current_stream().synchronize()
+        """Fresh parameters and optimizer state, enqueued on the engine stream."""
         _check(self.L.lrs_dipnet_init_params(self.h, ctypes.c_uint64(seed & (2**64 - 1)),
                                              ctypes.c_void_p(self.stream.cuda_stream)), "init_params")
-        self.stream.synchronize()
 
     def param_views(self, i: int, flat=None):
         """(weight [cout,cin,k,k], bias, gamma|None, beta|None) views into `flat` (default params)."""
@@ -220,14 +218,20 @@ class EarlyStopper:
         nbytes = ctypes.sizeof(EsState)
         self.state = torch.zeros((nbytes + 7) // 8, dtype=torch.float64, device=device)
         self.ring = torch.zeros(size * n_elems, dtype=torch.float32, device=device)
+        self._host = None
         L = _lib.device_lib()
         _check(L.lrs_es_init(_ptr(self.state), size, patience, None), "lrs_es_init")
 
-    def read(self) -> EsState:
+    def read(self, stream=None) -> EsState:
+        """Copy the state to the host after the work queued on `stream` (default: current)."""
         import torch
-        torch.cuda.synchronize()
-        raw = self.state.cpu().numpy().tobytes()[:ctypes.sizeof(EsState)]
-        return EsState.from_buffer_copy(raw)
+        s = stream or torch.cuda.current_stream()
+        if self._host is None:
+            self._host = torch.empty(self.state.numel(), dtype=torch.float64, pin_memory=True)
+        with torch.cuda.stream(s):
+            self._host.copy_(self.state, non_blocking=True)
+        s.synchronize()
+        return EsState.from_buffer_copy(self._host.numpy().tobytes()[:ctypes.sizeof(EsState)])
 
     def slot_of(self, epoch: int):
         return self.ring.view(self.size, self.n)[epoch % self.size]
@@ -263,31 +267,41 @@ class LipschitzDip:
     def run(self, target, dip_input, mask, seed: int | None = None, num_iter: int | None = None,
             early_stop: bool = True):
         """Train a freshly initialised net on (dip_input -> target under mask) and return the output
-        at the early-stopping epoch (or after num_iter steps with early_stop=False)."""
+        at the early-stopping epoch (or after num_iter steps with early_stop=False).
+
+        The result is a view of an engine buffer, valid until the next call; it is ordered after
+        the caller's current stream (the caller's stream waits for the DIP stream on return)."""
         import torch
         cfg = self.cfg
         n_iter = cfg.num_iter if num_iter is None else num_iter
-        self.net.init_params(self.calls if seed is None else seed)
+        net = self.net
+        net.stream.wait_stream(torch.cuda.current_stream())
+        net.init_params(self.calls if seed is None else seed)
         self.calls += 1
         if not early_stop:
-            self.net.train_steps(dip_input, target, mask, n_iter, cfg.learning_rate, use_graph=cfg.use_graph)
+            net.train_steps(dip_input, target, mask, n_iter, cfg.learning_rate, use_graph=cfg.use_graph)
             self.last_steps, self.last_stop_epoch = n_iter, None
-            return self.net.output().clone()       # the last step's forward output (`out`)
+            return net.output()                    # the last step's forward output (`out`)
         L = _lib.device_lib()
-        _check(L.lrs_es_init(_ptr(self.es.state), cfg.es_size, cfg.patience, None), "lrs_es_init")
+        _check(L.lrs_es_init(_ptr(self.es.state), cfg.es_size, cfg.patience, ctypes.c_void_p(net.stream.cuda_stream)),
+               "lrs_es_init")
         done = 0
+        st = None
         while done < n_iter:
             k = min(cfg.poll_every, n_iter - done)
-            self.net.train_steps(dip_input, target, mask, k, cfg.learning_rate, es=self.es, use_graph=cfg.use_graph)
+            net.train_steps(dip_input, target, mask, k, cfg.learning_rate, es=self.es, use_graph=cfg.use_graph)
             done += k
-            st = self.es.read()
+            st = self.es.read(net.stream)
             if st.stop:
-                self.last_steps, self.last_stop_epoch = done, st.stop_epoch
-                return self.es.slot_of(st.stop_epoch).view(self.net.out_shape).clone()
-        self.last_steps, self.last_stop_epoch = done, None
-        # the reference returns None here (the loop ends without returning); return the last output
-        st = self.es.read()
-        return self.es.slot_of(st.count - 1).view(self.net.out_shape).clone()
+                break
+        torch.cuda.current_stream().wait_stream(net.stream)
+        self.last_steps = done
+        if st is not None and st.stop:
+            self.last_stop_epoch = st.stop_epoch
+            return self.es.slot_of(st.stop_epoch).view(net.out_shape)
+        # the reference returns None here (its loop ends without returning); use the last output
+        self.last_stop_epoch = None
+        return self.es.slot_of(st.count - 1).view(net.out_shape)
 
 
 def dip_input_from_unfolded(Z, H: int, W: int):

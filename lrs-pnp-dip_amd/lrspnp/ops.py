@@ -14,7 +14,7 @@ from ._lib import (ALPHA_FRO4, ALPHA_SOFT, ALPHA_SPEC2, PROX_NLM, PROX_SOFT, Lrs
                    device_lib, lib)
 
 __all__ = ["nlm_col", "block_grid", "cover_ranges", "im2col", "ista_alpha", "ista", "svt_workspace",
-           "svt", "admm_update", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT"]
+           "svt", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT"]
 
 
 def _p(t):
@@ -188,3 +188,26 @@ def admm_update(X, L1, L2, Y, M, U, phi, bb, grid, gamma, mu1, mu2, norms=None, 
                                 _p(grid["rstarts"]), _p(grid["cstarts"]), grid["nbr"], _p(grid["rlo"]),
                                 _p(grid["rhi"]), _p(grid["clo"]), _p(grid["chi"]), float(gamma), float(mu1),
                                 float(mu2), _p(norms), _p(imout), _s(stream)), "lrs_admm_update_f32")
+
+
+def unfolded_to_image(X, L, c: float, H: int, W: int, out=None, stream=None):
+    """img[b][i][j] = X[i + H j][b] + c * L[...]   (…1-LiP.py:404 DIP_input layout)."""
+    Ld = device_lib()
+    _dev(X, torch.float32, "X")
+    P, B = X.shape
+    if P != H * W:
+        raise LrsError(f"P = {P} != H*W = {H * W}")
+    out = out if out is not None else torch.empty((B, H, W), dtype=torch.float32, device=X.device)
+    check(Ld.lrs_unfolded_to_image_f32(_p(X), _p(L), ctypes.c_float(c), H, W, B, _p(out), _s(stream)),
+          "lrs_unfolded_to_image_f32")
+    return out
+
+
+def image_to_unfolded(img, H: int, W: int, out=None, stream=None):
+    """X[i + H j][b] = img[b][i][j]   (…1-LiP.py:411 U layout)."""
+    Ld = device_lib()
+    _dev(img, torch.float32, "img")
+    B = img.numel() // (H * W)
+    out = out if out is not None else torch.empty((H * W, B), dtype=torch.float32, device=img.device)
+    check(Ld.lrs_image_to_unfolded_f32(_p(img), H, W, B, _p(out), _s(stream)), "lrs_image_to_unfolded_f32")
+    return out

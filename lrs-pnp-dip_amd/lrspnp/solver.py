@@ -32,11 +32,16 @@ class LrsPnPConfig:
     sliding: int = 36             # slidingDis                          :238
     variant: str = "spec2"        # 'spec2' (main), 'fro4' (DIP mains), 'soft' (ista.m)
     svt_warm: bool = True         # warm-start the Jacobi eigensolver from the previous iteration
+    lowrank: str = "svt"          # 'svt' (main_LRS_PnP.py:315) or 'dip' (…1-LiP.py:399-411)
+    dip: object = None            # lrspnp.dip.DipConfig for lowrank='dip' (None: reference defaults)
+    dip_seed: int = 0             # DIP init seed of outer iteration t is dip_seed + t
 
     @staticmethod
     def dip_1lip(**kw) -> "LrsPnPConfig":
-        """Parameters of main_LRS_PnP_DIP_1-LiP.py:316-333 (SVT stands in for the DIP prox)."""
-        base = dict(gamma=0.5, mu1=0.1, mu2=0.1, lambda_ista=0.1, Nit=100, bb=36, sliding=36, variant="fro4")
+        """Parameters of main_LRS_PnP_DIP_1-LiP.py:316-345: fro4 ISTA (Nit 100), mu1 = mu2 = 0.1,
+        and the 1-Lipschitz U-Net DIP as the low-rank prox."""
+        base = dict(gamma=0.5, mu1=0.1, mu2=0.1, lambda_ista=0.1, Nit=100, bb=36, sliding=36, variant="fro4",
+                    lowrank="dip")
         base.update(kw)
         return LrsPnPConfig(**base)
 
@@ -51,7 +56,7 @@ class LrsPnP:
     dictionary with n = bb*bb.  All float32 (numpy or torch); copied to the device once.
     """
 
-    def __init__(self, Y, M, D, cfg: LrsPnPConfig | None = None, device="cuda"):
+    def __init__(self, Y, M, D, cfg: LrsPnPConfig | None = None, device="cuda", image_shape=None):
         self.cfg = cfg = cfg or LrsPnPConfig()
         dev = torch.device(device)
         f = lambda a: torch.as_tensor(np.asarray(a, np.float32) if not isinstance(a, torch.Tensor) else a,
@@ -105,9 +110,33 @@ class LrsPnP:
         self.Yb = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
         self.phi = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
         self.norms = torch.zeros(3, dtype=torch.float64, device=dev)
-        self.svt_ws = ops.svt_workspace(self.P, self.B, dev)
         self.lowrank_stream = torch.cuda.Stream(device=dev)
         self.iteration = 0
+        self.dip = None
+        if cfg.lowrank == "svt":
+            self.svt_ws = ops.svt_workspace(self.P, self.B, dev)
+        elif cfg.lowrank == "dip":
+            self._init_dip(image_shape, dev)
+        else:
+            raise LrsError(f"unknown lowrank prox {cfg.lowrank!r}")
+
+    def _init_dip(self, image_shape, dev):
+        """DIP target = the observed cube as an image, mask_bkg = the pixel mask
+        (…1-LiP.py:275-301); the network is re-initialised every outer iteration (:214)."""
+        from .dip import DipConfig, LipschitzDip
+        if image_shape is None:
+            raise LrsError("lowrank='dip' needs image_shape=(H, W) with H*W = P")
+        H, W = (int(v) for v in image_shape)
+        if H * W != self.P:
+            raise LrsError(f"image_shape {H}x{W} does not match P = {self.P}")
+        self.H, self.W = H, W
+        self.dip = LipschitzDip(self.B, H, W, self.cfg.dip or DipConfig(), device=dev)
+        self.dip_target = torch.empty((self.B, H, W), dtype=torch.float32, device=dev)
+        ops.unfolded_to_image(self.Y, None, 1.0, H, W, self.dip_target)
+        pix = ops.unfolded_to_image(self.M[:, :1].contiguous(), None, 1.0, H, W)   # (1, H, W)
+        self.dip_mask = pix.reshape(-1).contiguous()
+        self.dip_in = torch.empty_like(self.dip_target)
+        self.dip_steps = []
 
     # -----------------------------------------------------------------------------------------
     def sparse_coding(self, stream=None, want_coefs=False):
@@ -122,8 +151,19 @@ class LrsPnP:
         return ops.svt(self.X, self.L2, self.c2, self.tau, self.svt_ws, U=self.U, s_out=s_out, warm=warm,
                        stream=stream)
 
+    def low_rank_dip(self, stream):
+        """U = DIP(X + L2/mu2) (…1-LiP.py:399-411) on `stream`; the host polls early stopping."""
+        ops.unfolded_to_image(self.X, self.L2, self.c2, self.H, self.W, self.dip_in, stream=stream)
+        with torch.cuda.stream(stream):
+            img = self.dip.run(self.dip_target, self.dip_in, self.dip_mask, seed=self.cfg.dip_seed + self.iteration)
+            ops.image_to_unfolded(img, self.H, self.W, self.U, stream=stream)
+        self.dip_steps.append((self.dip.last_steps, self.dip.last_stop_epoch))
+
     def step(self):
-        """One outer ADMM iteration (main_LRS_PnP.py:250-366), stream-ordered, no host sync."""
+        """One outer ADMM iteration (main_LRS_PnP.py:250-366), stream-ordered.  No host sync in
+        the SVT mode; the DIP mode polls its early-stopping flag on the low-rank stream only."""
+        if self.dip is not None:
+            return self._step_dip()
         main = torch.cuda.current_stream()
         lr = self.lowrank_stream
         warm = self.cfg.svt_warm and self.iteration > 0
@@ -138,6 +178,21 @@ class LrsPnP:
         main.wait_event(gram_done)
         ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
                  stream=main)
+        main.wait_stream(lr)
+        ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
+                        self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)
+        self.iteration += 1
+
+    def _step_dip(self):
+        main = torch.cuda.current_stream()
+        lr = self.lowrank_stream
+        lr.wait_stream(main)
+        # sparse coding is enqueued first so it runs beside the DIP training
+        ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
+                   stream=main)
+        ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
+                 stream=main)
+        self.low_rank_dip(lr)
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
                         self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)

@@ -294,3 +294,44 @@ def test_lipschitz_dip_run_early_stop(L):
     assert dip.last_stop_epoch is None or dip.last_stop_epoch >= 89   # >= 30 + 60 - 1 steps
     out2 = dip.run(t.cuda(), x.cuda(), m.reshape(-1).cuda(), seed=3, num_iter=5, early_stop=False)
     assert torch.isfinite(out2).all()
+
+
+def test_layout_transforms_match_reference_reshapes(L):
+    from lrspnp import ops
+    g = np.random.default_rng(0)
+    H, W, B = 12, 7, 5
+    X = g.standard_normal((H * W, B)).astype(np.float32)
+    L2 = g.standard_normal((H * W, B)).astype(np.float32)
+    c2 = np.float32(1 / 0.1)
+    # …1-LiP.py:404  (X + (1/mu_2)*lambda_2).numpy().transpose(1,0).reshape((B,W,H)).transpose((0,2,1))
+    ref_in = (X + c2 * L2).transpose(1, 0).reshape((B, W, H)).transpose((0, 2, 1))
+    got = ops.unfolded_to_image(torch.from_numpy(X).cuda(), torch.from_numpy(L2).cuda(), float(c2), H, W)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref_in)
+    img = g.standard_normal((B, H, W)).astype(np.float32)
+    # :411  U.numpy().transpose(0,1,3,2).reshape(B,-1).transpose(1,0)
+    ref_U = img[None].transpose(0, 1, 3, 2).reshape(B, -1).transpose(1, 0)
+    got_U = ops.image_to_unfolded(torch.from_numpy(img).cuda(), H, W)
+    np.testing.assert_array_equal(got_U.cpu().numpy(), ref_U)
+
+
+def test_solver_dip_mode_runs(L, golden):
+    """One LRS-PnP-DIP(1-Lip) outer iteration on the native 36x36x128 data (img5 + lrs_mask):
+    fro4 ISTA (Nit 100) beside the DIP prox, then the X / dual update."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.data import mask_matrix, synthetic_dictionary, unfold
+    from lrspnp.dip import DipConfig
+    from lrspnp.metrics import mpsnr
+    d = golden("data_img5.npz")
+    noisy, clean, mask = d["noisy_img5"][0], d["clean_img5"][0], d["lrs_mask"]
+    Y, M = unfold(noisy), mask_matrix(mask, 128)
+    cfg = LrsPnPConfig.dip_1lip(dip=DipConfig(num_iter=300, poll_every=10))
+    s = LrsPnP(Y, M, synthetic_dictionary(1296, 256, 0), cfg, image_shape=(36, 36))
+    clean_d = torch.from_numpy(np.ascontiguousarray(clean)).cuda()
+    p0 = mpsnr(s.X, clean_d)
+    s.step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(s.X).all() and torch.isfinite(s.U).all()
+    steps, stop = s.dip_steps[0]
+    assert 90 <= steps <= 300
+    p1 = mpsnr(s.X, clean_d)
+    assert np.isfinite(p1) and p1 > p0 - 3.0
