@@ -160,13 +160,16 @@ int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float *w, const 
                        float *gx, float *gw, void *ws, size_t ws_bytes, void *stream);
 
 /* y = act(BN_lip(z)) with batch statistics (gamma == NULL: y = act(z)).  Saves mean / invstd
- * [C]; running stats (nullable) get the momentum update. */
+ * [C]; running stats (nullable) get the momentum update.  ws: lrs_bn_act_workspace bytes,
+ * zero-filled before its first use (it is left zeroed for the next call). */
+size_t lrs_bn_act_workspace(int C, int64_t P);
 int lrs_bn_act_fwd_f32(const float *z, float *y, const float *gamma, const float *beta, float *mean,
                        float *invstd, float *run_mean, float *run_var, int C, int64_t P, int act,
-                       float eps, float momentum, void *stream);
+                       float eps, float momentum, void *ws, size_t ws_bytes, void *stream);
 int lrs_bn_act_bwd_f32(const float *gy, const float *y, const float *z, const float *gamma,
                        const float *mean, const float *invstd, float *gz, float *ggamma,
-                       float *gbeta, float *gbias, int C, int64_t P, int act, void *stream);
+                       float *gbeta, float *gbias, int C, int64_t P, int act, void *ws, size_t ws_bytes,
+                       void *stream);
 
 /* sigma_max of n weight matrices W[i] (rows[i] x cols[i], min(rows, cols) <= 128; host arrays
  * of device pointers), exact to fp64 before the float32 rounding; scale = max(1, sigma/ln_lambda)

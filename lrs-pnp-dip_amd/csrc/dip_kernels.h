@@ -251,32 +251,71 @@ __global__ void k_col2im(const float *__restrict__ dcol, ConvGeom gm, float *__r
 }
 
 // ------------------------------------------------------------------------------------------
-// BatchNorm2d (train mode, batch 1) with the Lipschitz rescale, + LeakyReLU(0.2), fused.
-// One workgroup per channel; statistics in fp64 (two-pass).
+// Wave / block reductions.  Doubles go through DPP row operations (no LDS crossbar): after four
+// steps every 16-lane row holds its row sum, then readlane gathers the four rows.
 // ------------------------------------------------------------------------------------------
-constexpr int kBnThreads = 256;
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 
-__device__ __forceinline__ double block_sum_d(double v, double *red) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// sum over the 64 lanes, result uniform (fixed order: deterministic)
+__device__ __forceinline__ double wave_sum_d(double v) {
+    v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_d<0x141>(v);   // row_half_mirror
+    v += dpp_d<0x140>(v);   // row_mirror
+    return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
+// block sum; red must hold 2 * (blockDim/64) doubles; `parity` alternates between calls so a
+// single barrier suffices (the other half of red is still being read by slow waves)
+__device__ __forceinline__ double block_sum_d1(double v, double *red, int &parity) {
+    const int nw = blockDim.x >> 6;
+    v = wave_sum_d(v);
+    double *r = red + parity * nw;
+    if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = v;
     __syncthreads();
     double s = 0.0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+    for (int i = 0; i < nw; ++i) s += r[i];
+    parity ^= 1;
     return s;
 }
 
-// c = max(max|gamma_orig|, 1.0) (lipschitz_constraint_layer.py:93-97)
-__device__ float bn_lip_scale(const float *gamma, int C, double *red) {
+__device__ __forceinline__ double block_sum_d(double v, double *red) {
+    int parity = 0;
+    const double s = block_sum_d1(v, red, parity);
+    __syncthreads();
+    return s;
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm2d (train mode, batch 1) with the Lipschitz rescale, + activation.
+// Each channel is split over S workgroups (grid = S x C).  Statistics: per-workgroup fp64
+// partials, the last workgroup of a channel (atomic ticket, fixed summation order) finalises.
+// Forward = k_bn_stats + k_bn_apply; backward = k_bn_bwd_stats + k_bn_bwd_apply.
+// ------------------------------------------------------------------------------------------
+constexpr int kBnThreads = 256;
+
+// c = max(max|gamma_orig|, 1.0) (lipschitz_constraint_layer.py:93-97); whole block, C <= 4 * blockDim
+__device__ float bn_lip_scale(const float *gamma, int C, float *redf) {
     float m = 0.0f;
     for (int i = threadIdx.x; i < C; i += blockDim.x) m = fmaxf(m, fabsf(gamma[i]));
-    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_down(m, off, 64));
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) redf[threadIdx.x >> 6] = m;
     __syncthreads();
     float r = 0.0f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r = fmaxf(r, (float)red[i]);
-    __syncthreads();
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r = fmaxf(r, redf[i]);
     return fmaxf(r, 1.0f);
 }
 
@@ -293,104 +332,163 @@ __device__ __forceinline__ float act_bwd(float g, float y, int act) {
 }
 
 struct BnArgs {
-    const float *z;          // [C][P] conv output
-    float *y;                // [C][P] activation output (may alias z when !bn)
+    const float *z;              // [C][P] conv output
+    float *y;                    // [C][P] activation output (may alias z when !bn)
     const float *gamma, *beta;   // bn params (orig), null when !bn
-    float *mean, *invstd;    // [C] saved statistics
-    float *run_mean, *run_var;   // [C] running statistics (updated, momentum)
-    int C, P, bn, act;
+    float *mean, *invstd;        // [C] saved statistics
+    float *run_mean, *run_var;   // [C] running statistics (momentum update), nullable
+    double *part;                // [C][S][3] partials
+    int C, P, S, chunk, bn, act;
     float eps, momentum;
 };
 
-__global__ __launch_bounds__(kBnThreads) void k_bn_act_fwd(BnArgs a) {
-    __shared__ double red[kBnThreads / 64];
-    const int c = blockIdx.x;
+// partial sums of (z - K), (z - K)^2 over this workgroup's slice, K = z[c][0] (stable variance)
+__global__ __launch_bounds__(kBnThreads) void k_bn_stats(BnArgs a) {
+    __shared__ double red[2 * kBnThreads / 64];
+    const int c = blockIdx.y, sb = blockIdx.x;
     const float *z = a.z + (int64_t)c * a.P;
-    float *y = a.y + (int64_t)c * a.P;
-    if (!a.bn) {
-        for (int i = threadIdx.x; i < a.P; i += blockDim.x) y[i] = act_fwd(z[i], a.act);
-        return;
+    const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
+    const double K = (double)z[0];
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const double d = (double)z[i] - K;
+        s1 += d;
+        s2 += d * d;
     }
-    const float cs = bn_lip_scale(a.gamma, a.C, red);
-    double s = 0.0;
-    for (int i = threadIdx.x; i < a.P; i += blockDim.x) s += (double)z[i];
-    const double mean = block_sum_d(s, red) / a.P;
-    double q = 0.0;
-    for (int i = threadIdx.x; i < a.P; i += blockDim.x) {
-        const double d = (double)z[i] - mean;
-        q += d * d;
-    }
-    const double var = block_sum_d(q, red) / a.P;
-    const float m32 = (float)mean;
-    const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
-    const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
-    for (int i = threadIdx.x; i < a.P; i += blockDim.x) y[i] = act_fwd((z[i] - m32) * is32 * gm + bt, a.act);
+    int par = 0;
+    s1 = block_sum_d1(s1, red, par);
+    s2 = block_sum_d1(s2, red, par);
     if (threadIdx.x == 0) {
-        a.mean[c] = m32;
-        a.invstd[c] = is32;
-        if (a.run_mean) {
-            const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
-            a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
-            a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
-        }
+        double *pp = a.part + ((int64_t)c * a.S + sb) * 3;
+        pp[0] = s1;
+        pp[1] = s2;
     }
 }
 
+// every workgroup reduces its channel's partials (fixed order), then normalises its slice
+__global__ __launch_bounds__(kBnThreads) void k_bn_apply(BnArgs a) {
+    __shared__ float redf[kBnThreads / 64];
+    __shared__ float st_s[2];
+    const int c = blockIdx.y, sb = blockIdx.x;
+    const int64_t off = (int64_t)c * a.P;
+    const float *z = a.z + off;
+    float *y = a.y + off;
+    const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
+    if (!a.bn) {
+        for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) y[i] = act_fwd(z[i], a.act);
+        return;
+    }
+    const float cs = bn_lip_scale(a.gamma, a.C, redf);
+    if (threadIdx.x == 0) {
+        double t1 = 0.0, t2 = 0.0;
+        const double *q = a.part + (int64_t)c * a.S * 3;
+        for (int j = 0; j < a.S; ++j) { t1 += q[3 * j]; t2 += q[3 * j + 1]; }
+        const double m = t1 / a.P;
+        double var = t2 / a.P - m * m;
+        if (var < 0.0) var = 0.0;
+        const float m32 = (float)((double)a.z[off] + m);
+        const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
+        st_s[0] = m32;
+        st_s[1] = is32;
+        if (sb == 0) {
+            a.mean[c] = m32;
+            a.invstd[c] = is32;
+            if (a.run_mean) {
+                const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
+                a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
+                a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+            }
+        }
+    }
+    __syncthreads();
+    const float m32 = st_s[0], is32 = st_s[1];
+    const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) y[i] = act_fwd((z[i] - m32) * is32 * gm + bt, a.act);
+}
+
 struct BnBwdArgs {
-    const float *gy;         // [C][P] dL/dy
-    const float *y, *z;      // activation output, conv output
-    const float *gamma;      // bn gamma_orig (null when !bn)
+    const float *gy;             // [C][P] dL/dy
+    const float *y, *z;          // activation output, conv output
+    const float *gamma;          // bn gamma_orig (null when !bn)
     const float *mean, *invstd;
-    float *gz;               // [C][P] dL/dz (may alias gy)
-    float *ggamma, *gbeta;   // [C] grads of gamma_orig / beta_orig (null when !bn)
-    float *gbias;            // [C] grad of the conv bias = sum_p dL/dz
-    int C, P, bn, act;
+    float *gz;                   // [C][P] dL/dz (may alias gy)
+    float *ggamma, *gbeta;       // [C] grads of gamma_orig / beta_orig (null when !bn)
+    float *gbias;                // [C] grad of the conv bias = sum_p dL/dz
+    double *part;                // [C][S][3] partials
+    int C, P, S, chunk, bn, act;
 };
 
-__global__ __launch_bounds__(kBnThreads) void k_bn_act_bwd(BnBwdArgs a) {
-    __shared__ double red[kBnThreads / 64];
-    const int c = blockIdx.x;
+__global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
+    __shared__ double red[2 * kBnThreads / 64];
+    const int c = blockIdx.y, sb = blockIdx.x;
+    const int64_t off = (int64_t)c * a.P;
+    const float *gy = a.gy + off, *y = a.y + off, *z = a.z + off;
+    const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
+    double sg = 0.0, sgx = 0.0, sx = 0.0;
+    if (a.bn) {
+        const float m32 = a.mean[c], is32 = a.invstd[c];
+        for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+            const float g = act_bwd(gy[i], y[i], a.act);
+            const float xh = (z[i] - m32) * is32;
+            sg += (double)g;
+            sgx += (double)g * (double)xh;
+            sx += (double)xh;
+        }
+    } else {
+        for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) sg += (double)act_bwd(gy[i], y[i], a.act);
+    }
+    int par = 0;
+    sg = block_sum_d1(sg, red, par);
+    sgx = block_sum_d1(sgx, red, par);
+    sx = block_sum_d1(sx, red, par);
+    if (threadIdx.x == 0) {
+        double *pp = a.part + ((int64_t)c * a.S + sb) * 3;
+        pp[0] = sg;
+        pp[1] = sgx;
+        pp[2] = sx;
+    }
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_bn_bwd_apply(BnBwdArgs a) {
+    __shared__ float redf[kBnThreads / 64];
+    __shared__ float st_s[2];
+    const int c = blockIdx.y, sb = blockIdx.x;
     const int64_t off = (int64_t)c * a.P;
     const float *gy = a.gy + off, *y = a.y + off, *z = a.z + off;
     float *gz = a.gz + off;
+    const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
+    double t[3] = {0.0, 0.0, 0.0};
+    if (threadIdx.x == 0 && (a.bn || (sb == 0 && a.gbias))) {
+        const double *q = a.part + (int64_t)c * a.S * 3;
+        for (int j = 0; j < a.S; ++j)
+            for (int e = 0; e < 3; ++e) t[e] += q[3 * j + e];
+    }
     if (!a.bn) {
-        double s = 0.0;
-        for (int i = threadIdx.x; i < a.P; i += blockDim.x) {
-            const float g = act_bwd(gy[i], y[i], a.act);
-            gz[i] = g;
-            s += (double)g;
-        }
-        const double tot = block_sum_d(s, red);
-        if (threadIdx.x == 0 && a.gbias) a.gbias[c] = (float)tot;
+        if (threadIdx.x == 0 && sb == 0 && a.gbias) a.gbias[c] = (float)t[0];
+        for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) gz[i] = act_bwd(gy[i], y[i], a.act);
         return;
     }
-    const float cs = bn_lip_scale(a.gamma, a.C, red);
+    const float cs = bn_lip_scale(a.gamma, a.C, redf);
     const float m32 = a.mean[c], is32 = a.invstd[c];
-    double sg = 0.0, sgx = 0.0;
-    for (int i = threadIdx.x; i < a.P; i += blockDim.x) {
-        const float g = act_bwd(gy[i], y[i], a.act);
-        const float xh = (z[i] - m32) * is32;
-        sg += (double)g;
-        sgx += (double)g * (double)xh;
-    }
-    sg = block_sum_d(sg, red);
-    sgx = block_sum_d(sgx, red);
     const float gm = a.gamma[c] / cs;
-    const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
     const float k = gm * is32;
-    double sb = 0.0;
-    for (int i = threadIdx.x; i < a.P; i += blockDim.x) {
+    if (threadIdx.x == 0) {
+        const float mg = (float)(t[0] / a.P), mgx = (float)(t[1] / a.P);
+        st_s[0] = mg;
+        st_s[1] = mgx;
+        if (sb == 0) {
+            a.ggamma[c] = (float)t[1] / cs;
+            a.gbeta[c] = (float)t[0] / cs;
+            // conv bias grad = sum_p gz = k (sg - P mg - mgx sum_p xhat)  (zero in exact arithmetic)
+            if (a.gbias) a.gbias[c] = (float)((double)k * (t[0] - (double)a.P * mg - (double)mgx * t[2]));
+        }
+    }
+    __syncthreads();
+    const float mg = st_s[0], mgx = st_s[1];
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const float g = act_bwd(gy[i], y[i], a.act);
         const float xh = (z[i] - m32) * is32;
-        const float d = k * (g - mg - xh * mgx);
-        gz[i] = d;
-        sb += (double)d;
-    }
-    sb = block_sum_d(sb, red);
-    if (threadIdx.x == 0) {
-        a.ggamma[c] = (float)sgx / cs;
-        a.gbeta[c] = (float)sg / cs;
-        if (a.gbias) a.gbias[c] = (float)sb;
+        gz[i] = k * (g - mg - xh * mgx);
     }
 }
 
@@ -399,26 +497,29 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_act_bwd(BnBwdArgs a) {
 // Gram on the smaller side (m = min(rows, cols) <= 128) in fp64, exact products.
 // ------------------------------------------------------------------------------------------
 constexpr int kSnMaxDim = 128;
+constexpr int kSnSplit = 8;   // inner-dimension split of the Gram (partials summed in k_sn_sigma)
 
+// grid (tiles^2, kSnSplit, n): partial z of the Gram tile (ti, tj) over its inner range
 __global__ __launch_bounds__(256) void k_sn_gram(const SnConv *convs, double *gram) {
-    const SnConv cv = convs[blockIdx.y];
+    const SnConv cv = convs[blockIdx.z];
     const bool rowside = cv.rows <= cv.cols;    // G = W W^T (rows) or W^T W (cols)
     const int m = rowside ? cv.rows : cv.cols;
     const int inner = rowside ? cv.cols : cv.rows;
     const int tiles = (m + 31) / 32;
     if ((int)blockIdx.x >= tiles * tiles) return;
     const int ti = blockIdx.x / tiles, tj = blockIdx.x % tiles;
+    const int per = (int)round_up((inner + kSnSplit - 1) / kSnSplit, 32);
+    const int kb = blockIdx.y * per, ke = min(inner, kb + per);
     __shared__ float Si[32][33], Sj[32][33];
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 8 rows of 32
     double acc[4] = {0, 0, 0, 0};
-    double *G = gram + (int64_t)blockIdx.y * kSnMaxDim * kSnMaxDim;
-    for (int k0 = 0; k0 < inner; k0 += 32) {
-        // Si[r][kk] = V(ti*32 + r, k0 + kk) where V(i, k) = rowside ? W[i][k] : W[k][i]
+    double *G = gram + ((int64_t)blockIdx.z * kSnSplit + blockIdx.y) * kSnMaxDim * kSnMaxDim;
+    for (int k0 = kb; k0 < ke; k0 += 32) {
         for (int e = threadIdx.x; e < 32 * 32; e += 256) {
             const int r = e >> 5, kk = e & 31;
             const int ii = ti * 32 + r, jj = tj * 32 + r, k = k0 + kk;
             float vi = 0.f, vj = 0.f;
-            if (k < inner) {
+            if (k < ke) {
                 if (rowside) {
                     if (ii < m) vi = cv.W[(int64_t)ii * cv.cols + k];
                     if (jj < m) vj = cv.W[(int64_t)jj * cv.cols + k];
@@ -446,98 +547,150 @@ __global__ __launch_bounds__(256) void k_sn_gram(const SnConv *convs, double *gr
     }
 }
 
+// number of eigenvalues of the symmetric tridiagonal (diag al, squared off-diagonal be2) above x:
+// k minus the sign changes of the characteristic-polynomial sequence p_i = (al_i - x) p_{i-1}
+// - be2_{i-1} p_{i-2} (division-free; rescaled by a power of two every 8 terms)
 __device__ int sturm_gt(const double *al, const double *be2, int k, double x) {
-    int neg = 0;
-    double d = 1.0;
-    for (int i = 0; i < k; ++i) {
-        d = (al[i] - x) - (i > 0 ? be2[i - 1] / d : 0.0);
-        if (d == 0.0) d = -1e-300;
-        neg += d < 0.0;
+    double pm = 1.0, p = al[0] - x;
+    int changes = (p < 0.0) || (p == 0.0);   // p_0 = 1 > 0
+    for (int i = 1; i < k; ++i) {
+        const double pn = __fma_rn(al[i] - x, p, -be2[i - 1] * pm);
+        // sign change between p_{i-1} and p_i (a zero takes the sign opposite to its predecessor)
+        const bool neg_prev = (p < 0.0) || (p == 0.0 && pm > 0.0);
+        const bool neg_cur = (pn < 0.0) || (pn == 0.0 && !neg_prev);
+        changes += neg_prev != neg_cur;
+        pm = p;
+        p = pn;
+        if ((i & 7) == 7) {
+            int e;
+            frexp(fabs(p) > fabs(pm) ? p : pm, &e);
+            p = ldexp(p, -e);
+            pm = ldexp(pm, -e);
+        }
     }
-    return k - neg;
+    return k - changes;
 }
 
-// One workgroup (256 threads) per conv: Lanczos (no reorthogonalisation: the extreme Ritz value
-// converges regardless, Paige) run for m steps with the Gram in registers (thread t holds half a
-// row, 64 doubles), then a 256-point multisection of the tridiagonal for lambda_max.
-// sigma32 = float(sqrt(lambda_max)); scale = max(1, sigma32 / ln_lambda) (float32, as torch).
-__global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const double *gram, float *sigma,
-                                                  float *scale, float ln_lambda) {
-    const SnConv cv = convs[blockIdx.x];
-    const int m = cv.rows <= cv.cols ? cv.rows : cv.cols;
-    const double *G = gram + (int64_t)blockIdx.x * kSnMaxDim * kSnMaxDim;
-    __shared__ double q[kSnMaxDim], al[kSnMaxDim], be2[kSnMaxDim], red[8];
-    __shared__ double lo_s, hi_s;
-    __shared__ int best_s;
-    const int t = threadIdx.x, row = t >> 1, half = t & 1;
-    double g[64];
-#pragma unroll
-    for (int c = 0; c < 64; ++c) {
-        const int col = half * 64 + c;
-        g[c] = (row < m && col < m) ? G[row * kSnMaxDim + col] : 0.0;
-    }
-    // q0 = normalised deterministic start vector
-    double qr = 0.0, qprev = 0.0, wr;
-    if (row < m) qr = 1.0 + 0.5 * sin(0.7 * (double)row + 0.3);
-    {
-        const double nn = block_sum_d(half == 0 ? qr * qr : 0.0, red);
-        qr = qr / sqrt(nn);
-    }
-    if (half == 0) q[row] = qr;
-    __syncthreads();
-    double beta = 0.0;
-    int k = 0;
-    for (; k < m; ++k) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < 64; ++c) s = __fma_rn(g[c], q[half * 64 + c], s);
-        s += __shfl_xor(s, 1, 64);
-        wr = s;                                   // (G q)_row, both halves
-        const double a = block_sum_d(half == 0 ? qr * wr : 0.0, red);
-        wr = wr - a * qr - beta * qprev;
-        const double b2 = block_sum_d(half == 0 ? wr * wr : 0.0, red);
-        if (t == 0) { al[k] = a; be2[k] = b2; }
-        const double b = sqrt(b2);
-        if (!(b > 1e-14 * fabs(a)) || k + 1 == m) { ++k; break; }
-        qprev = qr;
-        qr = wr / b;
-        beta = b;
-        __syncthreads();                          // all reads of q done
-        if (half == 0) q[row] = qr;
-        __syncthreads();
-    }
-    __syncthreads();
-    // Gershgorin interval of T_k, then multisection
+// Largest eigenvalue of the symmetric tridiagonal T_k (diag al, off-diagonal be, be2 = be^2):
+// Gershgorin interval, then `rounds` 256-point multisections (each narrows it 257x).  Whole
+// block; result uniform.
+__device__ double tridiag_max_eig(const double *al, const double *be, const double *be2, int k, int rounds,
+                                  double *lohi, int *best) {
+    const int t = threadIdx.x;
     if (t == 0) {
         double lo = 1e300, hi = -1e300;
         for (int i = 0; i < k; ++i) {
-            const double r = (i > 0 ? sqrt(be2[i - 1]) : 0.0) + (i + 1 < k ? sqrt(be2[i]) : 0.0);
+            const double r = (i > 0 ? be[i - 1] : 0.0) + (i + 1 < k ? be[i] : 0.0);
             lo = fmin(lo, al[i] - r);
             hi = fmax(hi, al[i] + r);
         }
-        lo_s = fmax(lo, 0.0);
-        hi_s = hi;
+        lohi[0] = fmax(lo, 0.0);
+        lohi[1] = hi;
     }
     __syncthreads();
-    for (int round = 0; round < 10; ++round) {
-        const double lo = lo_s, hi = hi_s;
-        if (!(hi - lo > 0.0)) break;
+    for (int round = 0; round < rounds; ++round) {
+        const double lo = lohi[0], hi = lohi[1];
+        if (!(hi - lo > 1e-15 * hi)) break;
         const double x = lo + (hi - lo) * (double)(t + 1) / 257.0;
-        if (t == 0) best_s = -1;
+        if (t == 0) *best = -1;
         __syncthreads();
-        if (x > lo && x < hi && sturm_gt(al, be2, k, x) >= 1) atomicMax(&best_s, t);
+        if (x > lo && x < hi && sturm_gt(al, be2, k, x) >= 1) atomicMax(best, t);
         __syncthreads();
         if (t == 0) {
-            const int bt = best_s;
+            const int bt = *best;
             const double nlo = bt >= 0 ? lo + (hi - lo) * (double)(bt + 1) / 257.0 : lo;
             const double nhi = bt + 1 <= 255 ? lo + (hi - lo) * (double)(bt + 2) / 257.0 : hi;
-            lo_s = nlo;
-            hi_s = fmax(nlo, nhi);
+            lohi[0] = nlo;
+            lohi[1] = fmax(nlo, nhi);
         }
         __syncthreads();
     }
+    return 0.5 * (lohi[0] + lohi[1]);
+}
+
+// One workgroup (256 threads) per conv: Lanczos (no reorthogonalisation: the extreme Ritz value
+// converges regardless, Paige) with the Gram in registers (thread t holds half a row, 64
+// doubles).  Every 8 steps from step 16 the largest Ritz value is located to ~1e-10 (4
+// multisection rounds); the iteration stops when it moved less than 1e-11 relative (typically
+// 30-40 steps for these weights instead of m = 128), then 8 rounds pin lambda_max.
+// sigma32 = float(sqrt(lambda_max)); scale = max(1, sigma32 / ln_lambda) (float32, as torch).
+__global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const double *gram, float *sigma,
+                                                  float *scale, float ln_lambda, long long *prof) {
+    if (prof && threadIdx.x == 0) prof[blockIdx.x * 8 + 0] = wall_clock64();
+    const SnConv cv = convs[blockIdx.x];
+    const int m = cv.rows <= cv.cols ? cv.rows : cv.cols;
+    const double *G = gram + (int64_t)blockIdx.x * kSnSplit * kSnMaxDim * kSnMaxDim;
+    extern __shared__ double Gs[];                // [kSnMaxDim][kSnMaxDim + 1] (dynamic, 129 KB)
+    __shared__ double q[kSnMaxDim], al[kSnMaxDim], be[kSnMaxDim], be2[kSnMaxDim], lohi[2];
+    __shared__ int best_s;
+    const int t = threadIdx.x, row = t >> 1, half = t & 1;
+    // sum the split-K partials with coalesced loads into LDS, then each thread takes half a row
+    for (int e = t; e < kSnMaxDim * kSnMaxDim; e += blockDim.x) {
+        const int r = e / kSnMaxDim, c = e % kSnMaxDim;
+        double v = 0.0;
+        if (r < m && c < m)
+            for (int z = 0; z < kSnSplit; ++z) v += G[(int64_t)z * kSnMaxDim * kSnMaxDim + e];
+        Gs[r * (kSnMaxDim + 1) + c] = v;
+    }
+    __syncthreads();
+    double g[64];
+#pragma unroll
+    for (int c = 0; c < 64; ++c) g[c] = Gs[row * (kSnMaxDim + 1) + half * 64 + c];
+    if (prof && t == 0) prof[blockIdx.x * 8 + 1] = wall_clock64();
+    int par = 0;
+    // Lanczos on the unnormalised residual r_k (r_0 = start vector): one matvec u' = G r_k, one
+    // two-value reduction (||r_k||^2, r_k.u'), then beta_k = ||r_k||, q_k = r_k / beta_k,
+    // alpha_k = r_k.u' / beta_k^2 and r_{k+1} = u'/beta_k - alpha_k q_k - beta_k q_{k-1}.
+    // Two barriers per step.
+    double rr = (row < m) ? 1.0 + 0.5 * sin(0.7 * (double)row + 0.3) : 0.0;
+    double qprev = 0.0, theta_prev = -1.0;
+    __shared__ double red2[2][8];
+    if (half == 0) q[row] = rr;
+    __syncthreads();
+    int k = 0;
+    for (; k < m; ++k) {
+        double acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};    // 8 independent FMA chains
+#pragma unroll
+        for (int c = 0; c < 64; ++c) acc8[c & 7] = __fma_rn(g[c], q[half * 64 + c], acc8[c & 7]);
+        double u = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+        u += __shfl_xor(u, 1, 64);
+        const double w_rr = wave_sum_d(half == 0 ? rr * rr : 0.0);
+        const double w_ru = wave_sum_d(half == 0 ? rr * u : 0.0);
+        if ((t & 63) == 0) {
+            red2[0][(t >> 6) + 4 * par] = w_rr;
+            red2[1][(t >> 6) + 4 * par] = w_ru;
+        }
+        __syncthreads();
+        const double s_rr = (red2[0][4 * par] + red2[0][4 * par + 1]) + (red2[0][4 * par + 2] + red2[0][4 * par + 3]);
+        const double s_ru = (red2[1][4 * par] + red2[1][4 * par + 1]) + (red2[1][4 * par + 2] + red2[1][4 * par + 3]);
+        par ^= 1;
+        const double b = sqrt(s_rr);
+        if (k > 0 && !(b > 1e-14 * fabs(al[k - 1]))) break;   // invariant subspace: T_k is exact
+        const double ib = 1.0 / b;
+        const double a = s_ru * ib * ib;
+        if (t == 0) {
+            al[k] = a;
+            if (k > 0) { be[k - 1] = b; be2[k - 1] = s_rr; }
+        }
+        const double qk = rr * ib;
+        rr = u * ib - a * qk - (k > 0 ? b : 0.0) * qprev;
+        qprev = qk;
+        if (k + 1 == m) { ++k; break; }
+        if (k + 1 >= 24 && ((k + 1) & 7) == 0) {
+            __syncthreads();
+            const double th = tridiag_max_eig(al, be, be2, k + 1, 4, lohi, &best_s);
+            const bool conv = fabs(th - theta_prev) <= 1e-11 * th;
+            theta_prev = th;
+            if (conv) { ++k; break; }
+        }
+        if (half == 0) q[row] = rr;                   // the matvec reads of q finished before the barrier
+        __syncthreads();
+    }
+    __syncthreads();
+    if (prof && t == 0) { prof[blockIdx.x * 8 + 2] = wall_clock64(); prof[blockIdx.x * 8 + 4] = k; }
+    const double lmax = m > 0 ? tridiag_max_eig(al, be, be2, k, 8, lohi, &best_s) : 0.0;
+    if (prof && t == 0) prof[blockIdx.x * 8 + 3] = wall_clock64();
     if (t == 0) {
-        const double lmax = m > 0 ? 0.5 * (lo_s + hi_s) : 0.0;
         const float s32 = (float)sqrt(fmax(lmax, 0.0));
         sigma[blockIdx.x] = s32;
         scale[blockIdx.x] = fmaxf(1.0f, s32 / ln_lambda);
@@ -560,7 +713,7 @@ __global__ void k_sn_apply(const SnConv *convs, const float *scale) {
 __global__ void k_masked_mse(const float *__restrict__ out, const float *__restrict__ target,
                              const float *__restrict__ mask, int C, int64_t P, float *__restrict__ gout,
                              double *loss_acc) {
-    __shared__ double red[4];
+    __shared__ double red[8];
     const int64_t N = (int64_t)C * P;
     const float norm = (float)(2.0 / (double)N);
     double s = 0.0;
@@ -615,7 +768,7 @@ __global__ void k_es_push(const float *__restrict__ out, int64_t N, float *__res
 }
 
 __global__ void k_es_var(const float *__restrict__ ring, int64_t N, lrs_es_state *st) {
-    __shared__ double red[4];
+    __shared__ double red[8];
     if (st->count + 1 < st->size) return;   // count is incremented by k_es_decide
     const int S = st->size;
     double s = 0.0;

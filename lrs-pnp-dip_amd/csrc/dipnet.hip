@@ -139,28 +139,48 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
     return LRS_OK;
 }
 
+// workgroups per channel for the BN kernels: ~4096 elements each, at most 64
+inline int bn_split(int64_t P) {
+    int64_t S = (P + 4095) / 4096;
+    if (S < 1) S = 1;
+    if (S > 64) S = 64;
+    return (int)S;
+}
+
+inline int64_t bn_part_doubles(int C, int64_t P) { return (int64_t)C * bn_split(P) * 3; }
+
 int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, float *mean, float *invstd, float *rm,
-           float *rv, int C, int64_t P, int act, float eps, float mom, hipStream_t st) {
-    BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, C, (int)P, gamma ? 1 : 0, act, eps, mom};
-    hipLaunchKernelGGL(k_bn_act_fwd, dim3(C), dim3(kBnThreads), 0, st, a);
+           float *rv, int C, int64_t P, int act, float eps, float mom, double *part, hipStream_t st) {
+    const int S = bn_split(P);
+    const int chunk = (int)((P + S - 1) / S);
+    BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, part, C, (int)P, S, chunk, gamma ? 1 : 0, act, eps, mom};
+    if (gamma) hipLaunchKernelGGL(k_bn_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
+    hipLaunchKernelGGL(k_bn_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
 
 int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, const float *mean,
            const float *invstd, float *gz, float *ggamma, float *gbeta, float *gbias, int C, int64_t P, int act,
-           hipStream_t st) {
-    BnBwdArgs a{gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, C, (int)P, gamma ? 1 : 0, act};
-    hipLaunchKernelGGL(k_bn_act_bwd, dim3(C), dim3(kBnThreads), 0, st, a);
+           double *part, hipStream_t st) {
+    const int S = bn_split(P);
+    const int chunk = (int)((P + S - 1) / S);
+    BnBwdArgs a{gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, part, C, (int)P, S, chunk,
+                gamma ? 1 : 0, act};
+    if (gamma || gbias) hipLaunchKernelGGL(k_bn_bwd_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
+    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
 
 int sn_launch(const SnConv *table_dev, int n, int64_t max_elems, double *gram, float *sigma, float *scale,
-              float ln_lambda, bool apply, hipStream_t st) {
+              float ln_lambda, bool apply, hipStream_t st, long long *prof = nullptr) {
     const int tiles = (kSnMaxDim + 31) / 32;
-    hipLaunchKernelGGL(k_sn_gram, dim3(tiles * tiles, n), dim3(256), 0, st, table_dev, gram);
-    hipLaunchKernelGGL(k_sn_sigma, dim3(n), dim3(256), 0, st, table_dev, gram, sigma, scale, ln_lambda);
+    hipLaunchKernelGGL(k_sn_gram, dim3(tiles * tiles, kSnSplit, n), dim3(256), 0, st, table_dev, gram);
+    const size_t lds = sizeof(double) * kSnMaxDim * (kSnMaxDim + 1);
+    hipError_t e = hipFuncSetAttribute((const void *)k_sn_sigma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_sn_sigma, dim3(n), dim3(256), lds, st, table_dev, gram, sigma, scale, ln_lambda, prof);
     if (apply) hipLaunchKernelGGL(k_sn_apply, dim3(ew_blocks(max_elems, 256), n), dim3(kEw), 0, st, table_dev, scale);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
@@ -288,25 +308,43 @@ extern "C" int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float
     return conv_bwd(g, gy, col, w, w_div, Cout, gx, gw, dc, pt, part, (hipStream_t)stream);
 }
 
+extern "C" size_t lrs_bn_act_workspace(int C, int64_t P) {
+    if (C <= 0 || P <= 0) return 0;
+    return (size_t)bn_part_doubles(C, P) * sizeof(double) + 256;
+}
+
+static int bn_ws(void *ws, size_t ws_bytes, int C, int64_t P, double **part) {
+    if (!ws || ws_bytes < lrs_bn_act_workspace(C, P)) return LRS_E_WORKSPACE;
+    *part = (double *)ws;
+    return LRS_OK;
+}
+
 extern "C" int lrs_bn_act_fwd_f32(const float *z, float *y, const float *gamma, const float *beta, float *mean,
                                   float *invstd, float *run_mean, float *run_var, int C, int64_t P, int act,
-                                  float eps, float momentum, void *stream) {
+                                  float eps, float momentum, void *ws, size_t ws_bytes, void *stream) {
     if (!z || !y || C <= 0 || P <= 0 || P > INT32_MAX) return LRS_E_INVALID;
     if (gamma && (!beta || !mean || !invstd)) return LRS_E_INVALID;
-    return bn_fwd(z, y, gamma, beta, mean, invstd, run_mean, run_var, C, P, act, eps, momentum, (hipStream_t)stream);
+    double *part;
+    const int rc = bn_ws(ws, ws_bytes, C, P, &part);
+    if (rc) return rc;
+    return bn_fwd(z, y, gamma, beta, mean, invstd, run_mean, run_var, C, P, act, eps, momentum, part,
+                  (hipStream_t)stream);
 }
 
 extern "C" int lrs_bn_act_bwd_f32(const float *gy, const float *y, const float *z, const float *gamma,
                                   const float *mean, const float *invstd, float *gz, float *ggamma, float *gbeta,
-                                  float *gbias, int C, int64_t P, int act, void *stream) {
+                                  float *gbias, int C, int64_t P, int act, void *ws, size_t ws_bytes, void *stream) {
     if (!gy || !y || !gz || C <= 0 || P <= 0 || P > INT32_MAX) return LRS_E_INVALID;
     if (gamma && (!z || !mean || !invstd || !ggamma || !gbeta)) return LRS_E_INVALID;
-    return bn_bwd(gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, C, P, act, (hipStream_t)stream);
+    double *part;
+    const int rc = bn_ws(ws, ws_bytes, C, P, &part);
+    if (rc) return rc;
+    return bn_bwd(gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, C, P, act, part, (hipStream_t)stream);
 }
 
 extern "C" size_t lrs_sigma_max_workspace(int n) {
     if (n <= 0) return 0;
-    return (size_t)n * kSnMaxDim * kSnMaxDim * sizeof(double) + (size_t)n * sizeof(SnConv) + 256;
+    return (size_t)n * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double) + (size_t)n * sizeof(SnConv) + 256;
 }
 
 extern "C" int lrs_sigma_max_f32(const float *const *W, float *const *Wn, const int *rows, const int *cols, int n,
@@ -325,13 +363,31 @@ extern "C" int lrs_sigma_max_f32(const float *const *W, float *const *Wn, const 
         if (e > maxe) maxe = e;
     }
     double *gram = (double *)ws;
-    SnConv *tdev = (SnConv *)((char *)ws + (size_t)n * kSnMaxDim * kSnMaxDim * sizeof(double));
+    SnConv *tdev = (SnConv *)((char *)ws + (size_t)n * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double));
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemcpyAsync(tdev, tab.data(), sizeof(SnConv) * n, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return (int)e;
     e = hipStreamSynchronize(st);   // the host table is a local
     if (e != hipSuccess) return (int)e;
     return sn_launch(tdev, n, maxe, gram, sigma, scale, ln_lambda, Wn != nullptr, st);
+}
+
+// diagnostics: phase timestamps (wall_clock64 ticks) of the sigma kernel, 8 int64 per matrix:
+// [start, Gram loaded, Lanczos done, multisection done, Lanczos steps]
+extern "C" int lrs_diag_sigma_phases(const float *const *W, const int *rows, const int *cols, int n, void *ws,
+                                     size_t ws_bytes, long long *prof, void *stream) {
+    if (n <= 0 || !W || !prof) return LRS_E_INVALID;
+    if (!ws || ws_bytes < lrs_sigma_max_workspace(n) + 2 * n * sizeof(float)) return LRS_E_WORKSPACE;
+    std::vector<SnConv> tab(n);
+    for (int i = 0; i < n; ++i) tab[i] = SnConv{W[i], nullptr, rows[i], cols[i]};
+    double *gram = (double *)ws;
+    SnConv *tdev = (SnConv *)((char *)ws + (size_t)n * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double));
+    float *sig = (float *)((char *)ws + lrs_sigma_max_workspace(n));
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemcpyAsync(tdev, tab.data(), sizeof(SnConv) * n, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return (int)e;
+    return sn_launch(tdev, n, 0, gram, sig, sig + n, 1.0f, false, st, prof);
 }
 
 extern "C" int lrs_adam_f32(float *p, const float *g, float *m, float *v, int64_t n, const int *step, float lr,
@@ -400,6 +456,7 @@ struct lrs_dipnet {
     int64_t ws_floats = 0;
     int64_t ga_off = 0, gb_off = 0, dz_off = 0, dcol_off = 0, part_off = 0, part_cap = 0;
     int64_t sigma_off = 0, scale_off = 0, gram_off_bytes = 0, table_off_bytes = 0, misc_off_bytes = 0;
+    int64_t bnpart_off_bytes = 0, ticket_off_bytes = 0, ticket_bytes = 0;
     size_t ws_bytes = 0;
     int64_t max_w = 0;
     // bound buffers
@@ -419,6 +476,8 @@ struct lrs_dipnet {
     SnConv *table() const { return (SnConv *)(ws + table_off_bytes); }
     double *loss_acc() const { return (double *)(ws + misc_off_bytes); }
     int *step() const { return (int *)(ws + misc_off_bytes + 8); }
+    double *bnpart() const { return (double *)(ws + bnpart_off_bytes); }
+    int *ticket() const { return (int *)(ws + ticket_off_bytes); }
 };
 
 namespace {
@@ -441,7 +500,8 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
         if (rc) return rc;
         rc = bn_fwd(z, act, bn ? net->params + U.gm_off : nullptr, bn ? net->params + U.bt_off : nullptr,
                     net->f(U.mean_off), net->f(U.istd_off), bn ? net->bnstats + U.rs_off : nullptr,
-                    bn ? net->bnstats + U.rs_off + U.u.cout : nullptr, U.u.cout, U.P, U.u.act, 1e-5f, 0.1f, st);
+                    bn ? net->bnstats + U.rs_off + U.u.cout : nullptr, U.u.cout, U.P, U.u.act, 1e-5f, 0.1f,
+                    net->bnpart(), st);
         if (rc) return rc;
         src = act;
     }
@@ -469,7 +529,7 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
         float *gz = net->f(net->dz_off);
         rc = bn_bwd(g, act, z, bn ? net->params + U.gm_off : nullptr, net->f(U.mean_off), net->f(U.istd_off), gz,
                     bn ? net->grads + U.gm_off : nullptr, bn ? net->grads + U.bt_off : nullptr, net->grads + U.b_off,
-                    U.u.cout, U.P, U.u.act, st);
+                    U.u.cout, U.P, U.u.act, net->bnpart(), st);
         if (rc) return rc;
         const float *colsrc = U.col_off >= 0 ? net->f(U.col_off) : (i == 0 ? x : net->f(net->units[i - 1].act_off));
         rc = conv_bwd(U.g, gz, colsrc, net->f(U.wn_off), net->f(net->scale_off) + i, U.u.cout, i > 0 ? g2 : nullptr,
@@ -509,6 +569,7 @@ extern "C" int lrs_dipnet_create(const lrs_conv_unit *units, int n_units, int H,
     net->W = W;
     int cin = units[0].cin, h = H, w = W;
     int64_t pofs = 0, rofs = 0, ofs = 0, max_act = (int64_t)cin * H * W, max_dz = 0, max_dcol = 0, part = 0;
+    int64_t max_bnpart = 0, max_c = 0;
     for (int i = 0; i < n_units; ++i) {
         lrs_dipnet::Unit U{};
         U.u = units[i];
@@ -543,6 +604,8 @@ extern "C" int lrs_dipnet_create(const lrs_conv_unit *units, int n_units, int H,
         if (U.u.cout * U.Kc > net->max_w) net->max_w = U.u.cout * U.Kc;
         if (U.u.cout * U.P > max_act) max_act = U.u.cout * U.P;
         if (U.u.cout * U.P > max_dz) max_dz = U.u.cout * U.P;
+        if (bn_part_doubles(U.u.cout, U.P) > max_bnpart) max_bnpart = bn_part_doubles(U.u.cout, U.P);
+        if (U.u.cout > max_c) max_c = U.u.cout;
         const int64_t pc = conv_part_floats(U.g, U.u.cout);
         if (pc > part) part = pc;
         net->units.push_back(U);
@@ -563,7 +626,12 @@ extern "C" int lrs_dipnet_create(const lrs_conv_unit *units, int n_units, int H,
     net->ws_floats = ofs;
     size_t bytes = (size_t)ofs * sizeof(float);
     net->gram_off_bytes = (int64_t)bytes;
-    bytes += (size_t)n_units * kSnMaxDim * kSnMaxDim * sizeof(double);
+    bytes += (size_t)n_units * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double);
+    net->bnpart_off_bytes = (int64_t)bytes;
+    bytes += (size_t)round_up(max_bnpart * (int64_t)sizeof(double), 256);
+    net->ticket_off_bytes = (int64_t)bytes;
+    net->ticket_bytes = round_up(max_c * (int64_t)sizeof(int), 256);
+    bytes += (size_t)net->ticket_bytes;
     net->table_off_bytes = (int64_t)bytes;
     bytes += (size_t)round_up((int64_t)(n_units * sizeof(SnConv)), 256);
     net->misc_off_bytes = (int64_t)bytes;
@@ -623,6 +691,7 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
     hipError_t e = hipMemcpy(net->table(), tab.data(), sizeof(SnConv) * n, hipMemcpyHostToDevice);
     if (e != hipSuccess) return (int)e;
     e = hipMemset(net->misc_off_bytes + net->ws, 0, 256);
+    if (e == hipSuccess) e = hipMemset(net->ticket(), 0, (size_t)net->ticket_bytes);
     return e == hipSuccess ? LRS_OK : (int)e;
 }
 

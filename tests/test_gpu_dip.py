@@ -97,7 +97,8 @@ def test_conv_fwd_bwd(L, case):
     assert rel(gx, xr.grad) < 2e-5
 
 
-@pytest.mark.parametrize("bn,act,C,HW", [(1, 1, 128, 36 * 36), (1, 1, 64, 9), (0, 1, 198, 1296), (1, 2, 16, 100)])
+@pytest.mark.parametrize("bn,act,C,HW", [(1, 1, 128, 36 * 36), (1, 1, 64, 9), (0, 1, 198, 1296), (1, 2, 16, 100),
+                                         (1, 1, 128, 196 * 196), (0, 1, 8, 50000)])
 def test_bn_act(L, bn, act, C, HW):
     g = torch.Generator().manual_seed(C + HW)
     z = torch.randn(C, HW, generator=g) * 2 + 0.5
@@ -115,17 +116,22 @@ def test_bn_act(L, bn, act, C, HW):
     y = torch.empty_like(zd)
     mean, istd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
     rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    nws = L.lrs_bn_act_workspace(C, HW)
+    ws = torch.zeros(nws, dtype=torch.uint8, device="cuda")
     assert L.lrs_bn_act_fwd_f32(P(zd), P(y), P(gmd) if bn else None, P(btd) if bn else None, P(mean), P(istd),
                                 P(rm) if bn else None, P(rv) if bn else None, C, HW, act, ctypes.c_float(1e-5),
-                                ctypes.c_float(0.1), S()) == 0
+                                ctypes.c_float(0.1), P(ws), nws, S()) == 0
     assert rel(y, yr.detach()) < 1e-5
     gz = torch.empty_like(zd)
     gg, gb, gbias = torch.empty(C, device="cuda"), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
     assert L.lrs_bn_act_bwd_f32(P(gyd), P(y), P(zd), P(gmd) if bn else None, P(mean), P(istd), P(gz),
-                                P(gg) if bn else None, P(gb) if bn else None, P(gbias), C, HW, act, S()) == 0
+                                P(gg) if bn else None, P(gb) if bn else None, P(gbias), C, HW, act, P(ws), nws,
+                                S()) == 0
     torch.cuda.synchronize()
     assert rel(gz, zr.grad) < 2e-5
-    assert rel(gbias, zr.grad.sum(1)) < 1e-3 or float(zr.grad.sum(1).abs().max()) < 1e-4
+    # conv-bias grad = sum_p gz: ~0 under a BN (rounding noise), so held to the noise scale
+    gsum, gabs = zr.grad.double().sum(1), zr.grad.double().abs().sum(1)
+    assert bool(((gbias.cpu().double() - gsum).abs() <= 1e-5 * gabs + 1e-6).all())
     if bn:
         assert rel(gg, gr.grad) < 2e-5 and rel(gb, br.grad) < 2e-5
         var = z.double().var(1, unbiased=True)
