@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="pnp", choices=["pnp", "dip"],
+                    help="pnp: BASELINE configs[1] (the headline); dip: configs[2], LRS-PnP-DIP(1-Lip) on a "
+                         "196x196x198 cube (the 200x200 cube cropped to a size the U-Net maps onto itself)")
+    ap.add_argument("--dip-steps", type=int, default=100, help="DIP steps per outer iteration (ES off, §8d)")
     return ap.parse_args()
 
 
@@ -105,8 +109,78 @@ def cpu_baseline(Y, M, D, bb, nit, budget_s):
                       f"est. {t_iter:.1f}s per outer iteration"}
 
 
+def unet_flops_per_step(units, H, W):
+    """Algorithmic MFMA FLOPs of one DIP training step: forward convs + dW + dX (no dX of unit 0)."""
+    from lrspnp.dip import out_size
+    fwd = bwd = 0
+    h, w = H, W
+    for i, u in enumerate(units):
+        h, w = out_size(h, w, u.k, u.stride, u.pad, u.upsample)
+        f = 2 * u.cout * u.cin * u.k * u.k * h * w
+        fwd += f
+        bwd += f * (2 if i > 0 else 1)
+    return fwd + bwd
+
+
+def main_dip(args):
+    import torch
+
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp import dist as D
+    from lrspnp.dip import DipConfig, lipschitz_unet_units
+    from lrspnp.metrics import mpsnr
+    ctx = D.init_from_env("nccl")
+    H = W = 196
+    B = 198
+    bb = 36 if args.bb == 8 else args.bb
+    Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=ctx.rank)
+    dcfg = DipConfig(num_iter=args.dip_steps, early_stop=False)
+    cfg = LrsPnPConfig.dip_1lip(bb=bb, sliding=bb, dip=dcfg)
+    s = LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
+    clean_d = torch.from_numpy(clean).cuda()
+    mp0 = mpsnr(s.X, clean_d)
+    # DIP training time per outer iteration: events on the low-rank stream around the DIP call
+    ev = []
+    orig = s.low_rank_dip
+
+    def timed(stream):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        orig(stream)
+        e1.record(stream)
+        ev.append((e0, e1))
+
+    s.low_rank_dip = timed
+    elapsed = D.timed_steps(s.step, args.steps, args.warmup, ctx)
+    dip_ms = float(np.mean([a.elapsed_time(b) for a, b in ev[args.warmup:]]))
+    mp1 = mpsnr(s.X, clean_d)
+    flops = unet_flops_per_step(lipschitz_unet_units(B, B, 128), H, W) * args.dip_steps
+    achieved = flops / (dip_ms * 1e-3) / 1e12
+    out = {
+        "metric": METRIC, "value": ctx.world * args.steps / elapsed, "unit": "outer_iters/s",
+        "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32 (MFMA) + f64 (NLM, BN/sigma statistics)",
+        "data": "synthetic (seeded low-rank 196x196x198 cube per rank, random-init U-Net per outer iteration)",
+        "config": {"workload": f"LRS-PnP-DIP(1-Lip) 196x196x198, {bb}x{bb} blocks, K={args.K}, Nit=100 fro4 ISTA, "
+                               f"DIP my_Lipschitz_Unet (198->128->198 ch) {args.dip_steps} Adam steps, ES off "
+                               "(BASELINE configs[2])", "blocks": s.nb,
+                   "parallelism": f"{ctx.world} independent cube(s), one per GPU"},
+        "roofline": {"bound": "mfma", "kernel": "DIP training (conv GEMMs + BN/sigma/Adam kernels)",
+                     "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "flops_per_outer_iter": flops, "dip_ms_per_outer_iter": dip_ms},
+        "mpsnr": {"input": mp0, "after_steps": mp1, "steps_run": args.warmup + args.steps},
+    }
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "dip":
+        return main_dip(args)
     import torch
 
     from lrspnp import dist as D

@@ -32,10 +32,13 @@ namespace lrs {
 // GEMM  C[M][N] = op(A)[M][K] * op(B)[K][N]   (fp32, v_mfma_f32_16x16x4_f32)
 //   TA = 0: A stored [M][K];  TA = 1: A stored [K][M]
 //   TB = 0: B stored [K][N];  TB = 1: B stored [N][K]
-// 64x64 tile per 256-thread workgroup, BK = 16, each wave a 32x32 sub-tile (2x2 MFMA tiles).
+// 128x128 tile per 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA tiles), BK = 16.
+// Both operands sit in LDS k-contiguous ([x][BK+4] floats), so each lane fetches the four
+// k-steps of an MFMA fragment with one ds_read_b128; two LDS stages, one barrier per k-step,
+// the next k-step's global loads in flight during the MFMAs.
 // gridDim.z > 1 = split-K: partial z goes to Cpart + z*M*N and k_gemm_reduce finishes.
 // ------------------------------------------------------------------------------------------
-constexpr int kBM = 64, kBN = 64, kBK = 16, kGemmThreads = 256;
+constexpr int kBM = 128, kBN = 128, kBK = 16, kGemmThreads = 256, kLdsK = kBK + 4;
 
 struct GemmArgs {
     const float *A, *B;
@@ -45,10 +48,122 @@ struct GemmArgs {
     int M, N, K, kchunk;
 };
 
+// A 128(x) x 16(k) operand tile, 8 values per thread, as two float4 of 4 consecutive k.
+//  KCONTIG: stored [x][k] (k contiguous): thread -> x = t/2, k = 8 (t&1) + 0..7
+//  else   : stored [k][x] (x contiguous): thread -> x = t&127, k = 8 (t>>7) + 0..7
+template <bool KCONTIG>
+__device__ __forceinline__ void load_tile(const float *__restrict__ S, int ld, int k0, int kend, int x0, int X,
+                                          float4 (&r)[2]) {
+    const int t = threadIdx.x;
+    if (KCONTIG) {
+        const int x = x0 + (t >> 1), kb = k0 + 8 * (t & 1);
+        const float *src = S + (int64_t)x * ld;
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = (x < X && kb + u < kend) ? src[kb + u] : 0.0f;
+        r[0] = float4{v[0], v[1], v[2], v[3]};
+        r[1] = float4{v[4], v[5], v[6], v[7]};
+    } else {
+        const int x = x0 + (t & 127), kb = k0 + 8 * (t >> 7);
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = (x < X && kb + u < kend) ? S[(int64_t)(kb + u) * ld + x] : 0.0f;
+        r[0] = float4{v[0], v[1], v[2], v[3]};
+        r[1] = float4{v[4], v[5], v[6], v[7]};
+    }
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ void store_tile(float (*T)[kLdsK], const float4 (&r)[2]) {
+    const int t = threadIdx.x;
+    const int x = KCONTIG ? (t >> 1) : (t & 127);
+    const int kb = KCONTIG ? 8 * (t & 1) : 8 * (t >> 7);
+    *reinterpret_cast<float4 *>(&T[x][kb]) = r[0];
+    *reinterpret_cast<float4 *>(&T[x][kb + 4]) = r[1];
+}
+
+template <int TA, int TB>
+__global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) float As[2][kBM][kLdsK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][kBN][kLdsK];
+    const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+    const int kbeg = blockIdx.z * g.kchunk;
+    const int kend = min(g.K, kbeg + g.kchunk);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
+    const int jl = lane & 15, gk = lane >> 4;
+    const int lda = TA ? g.M : g.K;
+    const int ldb = TB ? g.K : g.N;
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float4 ra[2], rb[2];
+    load_tile<TA == 0>(g.A, lda, kbeg, kend, m0, g.M, ra);
+    load_tile<TB == 1>(g.B, ldb, kbeg, kend, n0, g.N, rb);
+    int stage = 0;
+    store_tile<TA == 0>(As[0], ra);
+    store_tile<TB == 1>(Bs[0], rb);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+        const bool more = k0 + kBK < kend;
+        if (more) {
+            load_tile<TA == 0>(g.A, lda, k0 + kBK, kend, m0, g.M, ra);
+            load_tile<TB == 1>(g.B, ldb, k0 + kBK, kend, n0, g.N, rb);
+        }
+        float4 fa[4], fb[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) fa[a] = *reinterpret_cast<const float4 *>(&As[stage][wm + 16 * a + jl][4 * gk]);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) fb[b] = *reinterpret_cast<const float4 *>(&Bs[stage][wn + 16 * b + jl][4 * gk]);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                acc[a][b] = mfma16x16x4(fa[a].x, fb[b].x, acc[a][b]);
+                acc[a][b] = mfma16x16x4(fa[a].y, fb[b].y, acc[a][b]);
+                acc[a][b] = mfma16x16x4(fa[a].z, fb[b].z, acc[a][b]);
+                acc[a][b] = mfma16x16x4(fa[a].w, fb[b].w, acc[a][b]);
+            }
+        if (more) {
+            store_tile<TA == 0>(As[stage ^ 1], ra);   // the other stage: last read one step ago
+            store_tile<TB == 1>(Bs[stage ^ 1], rb);
+        }
+        __syncthreads();
+        stage ^= 1;
+    }
+    float *C = g.C + (int64_t)blockIdx.z * g.M * g.N;
+    const bool final_out = gridDim.z == 1;
+    const float dv = (final_out && g.div) ? *g.div : 1.0f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int n = n0 + wn + 16 * b + jl;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + 16 * a + 4 * gk + r;
+                if (m < g.M && n < g.N) {
+                    float v = acc[a][b][r];
+                    if (final_out) {
+                        if (g.bias) v = v + g.bias[m];
+                        if (g.div) v = v / dv;
+                    }
+                    C[(int64_t)m * g.N + n] = v;
+                }
+            }
+        }
+}
+
+// ---- small-tile variant (64x64, BK 16, 2x2 waves of 32x32) for GEMMs whose 128-tile grid is
+// too small to fill the chip (the 36x36 native U-Net layers) ----------------------------------
+constexpr int kBM64 = 64, kBN64 = 64, kBK64 = 16;
+
 // Load a 16(k) x 64(x) operand tile into 4 registers per thread.
 //  kmajor = stored [k][x] (contiguous along x), else stored [x][k] (contiguous along k).
 template <bool KMAJOR>
-__device__ __forceinline__ void load_tile(const float *__restrict__ S, int ld, int k0, int kend, int x0, int X,
+__device__ __forceinline__ void load_tile64(const float *__restrict__ S, int ld, int k0, int kend, int x0, int X,
                                           float (&r)[4]) {
     const int t = threadIdx.x;
     if (KMAJOR) {
@@ -71,7 +186,7 @@ __device__ __forceinline__ void load_tile(const float *__restrict__ S, int ld, i
 }
 
 template <bool KMAJOR>
-__device__ __forceinline__ void store_tile(float (*T)[kBM + 4], const float (&r)[4]) {
+__device__ __forceinline__ void store_tile64(float (*T)[kBM64 + 4], const float (&r)[4]) {
     const int t = threadIdx.x;
     if (KMAJOR) {
         const int kk = t >> 4, i = (t & 15) * 4;
@@ -85,10 +200,10 @@ __device__ __forceinline__ void store_tile(float (*T)[kBM + 4], const float (&r)
 }
 
 template <int TA, int TB>
-__global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
-    __shared__ float As[kBK][kBM + 4];
-    __shared__ float Bs[kBK][kBN + 4];
-    const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+__global__ __launch_bounds__(kGemmThreads) void k_gemm64(GemmArgs g) {
+    __shared__ float As[kBK64][kBM64 + 4];
+    __shared__ float Bs[kBK64][kBN64 + 4];
+    const int m0 = blockIdx.y * kBM64, n0 = blockIdx.x * kBN64;
     const int kbeg = blockIdx.z * g.kchunk;
     const int kend = min(g.K, kbeg + g.kchunk);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -103,18 +218,18 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
     float ra[4], rb[4];
-    load_tile<TA == 1>(g.A, lda, kbeg, kend, m0, g.M, ra);
-    load_tile<TB == 0>(g.B, ldb, kbeg, kend, n0, g.N, rb);
-    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
-        store_tile<TA == 1>(As, ra);
-        store_tile<TB == 0>(Bs, rb);
+    load_tile64<TA == 1>(g.A, lda, kbeg, kend, m0, g.M, ra);
+    load_tile64<TB == 0>(g.B, ldb, kbeg, kend, n0, g.N, rb);
+    for (int k0 = kbeg; k0 < kend; k0 += kBK64) {
+        store_tile64<TA == 1>(As, ra);
+        store_tile64<TB == 0>(Bs, rb);
         __syncthreads();
-        if (k0 + kBK < kend) {
-            load_tile<TA == 1>(g.A, lda, k0 + kBK, kend, m0, g.M, ra);
-            load_tile<TB == 0>(g.B, ldb, k0 + kBK, kend, n0, g.N, rb);
+        if (k0 + kBK64 < kend) {
+            load_tile64<TA == 1>(g.A, lda, k0 + kBK64, kend, m0, g.M, ra);
+            load_tile64<TB == 0>(g.B, ldb, k0 + kBK64, kend, n0, g.N, rb);
         }
 #pragma unroll
-        for (int s = 0; s < kBK / 4; ++s) {
+        for (int s = 0; s < kBK64 / 4; ++s) {
             const float a0 = As[4 * s + gk][wm + jl], a1 = As[4 * s + gk][wm + 16 + jl];
             const float b0 = Bs[4 * s + gk][wn + jl], b1 = Bs[4 * s + gk][wn + 16 + jl];
             acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
@@ -147,14 +262,20 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
         }
 }
 
-// C = (sum_z part[z]) (+ bias[m]) (/ *div): fixed summation order (deterministic).
+// C = (sum_z part[z]) (+ bias[m]) (/ *div): fixed summation order (deterministic); 8 partial
+// chains so the loads of a long split stay in flight
 __global__ void k_gemm_reduce(const float *__restrict__ part, int nsplit, int M, int N, const float *bias,
                               const float *div, float *__restrict__ C) {
     const int64_t MN = (int64_t)M * N;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= MN) return;
-    float s = part[i];
-    for (int z = 1; z < nsplit; ++z) s += part[(int64_t)z * MN + i];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 8 <= nsplit; z += 8)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] += part[(int64_t)(z + u) * MN + i];
+    for (; z < nsplit; ++z) acc[z & 7] += part[(int64_t)z * MN + i];
+    float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     if (bias) s = s + bias[i / N];
     if (div) s = s / *div;
     C[i] = s;

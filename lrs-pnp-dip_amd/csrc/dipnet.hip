@@ -52,23 +52,28 @@ inline bool plain_unit(const ConvGeom &g) { return g.k == 1 && g.stride == 1 && 
 
 struct Split {
     int S, kchunk;
+    bool big;   // 128x128 tiles (k_gemm) or 64x64 (k_gemm64)
 };
 
-// split-K so that a GEMM launches ~1024 workgroups (4 per CU) when its tile grid is small
+// Tile choice and split-K: 128x128 tiles when they alone give >= 128 workgroups, else 64x64;
+// then split K until ~512 workgroups (2 per CU), keeping >= 128 of K per split and <= 64 splits.
 Split choose_split(int M, int N, int K) {
-    const int64_t tiles = (int64_t)((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+    const int64_t t128 = (int64_t)((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+    const bool big = t128 >= 128;
+    const int64_t tiles = big ? t128 : (int64_t)((M + kBM64 - 1) / kBM64) * ((N + kBN64 - 1) / kBN64);
     int S = 1;
-    if (tiles < 512) {
-        S = (int)((1024 + tiles - 1) / tiles);
-        const int smax = (K + 63) / 64;
+    if (tiles < 256) {
+        S = (int)((512 + tiles - 1) / tiles);
+        const int smax = (K + 127) / 128;
         if (S > smax) S = smax;
+        if (S > 64) S = 64;
         if (S < 1) S = 1;
     }
     int kchunk = (int)round_up((K + S - 1) / S, kBK);
     if (kchunk < kBK) kchunk = kBK;
     S = (K + kchunk - 1) / kchunk;
     if (S < 1) S = 1;
-    return {S, kchunk};
+    return {S, kchunk, big};
 }
 
 int64_t gemm_part_floats(int M, int N, int K) {
@@ -86,11 +91,19 @@ int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
         g.C = part;
     }
-    dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, s.S);
-    if (!TA && !TB) hipLaunchKernelGGL((k_gemm<0, 0>), grid, dim3(kGemmThreads), 0, st, g);
-    else if (!TA && TB) hipLaunchKernelGGL((k_gemm<0, 1>), grid, dim3(kGemmThreads), 0, st, g);
-    else if (TA && !TB) hipLaunchKernelGGL((k_gemm<1, 0>), grid, dim3(kGemmThreads), 0, st, g);
-    else hipLaunchKernelGGL((k_gemm<1, 1>), grid, dim3(kGemmThreads), 0, st, g);
+    if (s.big) {
+        dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, s.S);
+        if (!TA && !TB) hipLaunchKernelGGL((k_gemm<0, 0>), grid, dim3(kGemmThreads), 0, st, g);
+        else if (!TA && TB) hipLaunchKernelGGL((k_gemm<0, 1>), grid, dim3(kGemmThreads), 0, st, g);
+        else if (TA && !TB) hipLaunchKernelGGL((k_gemm<1, 0>), grid, dim3(kGemmThreads), 0, st, g);
+        else hipLaunchKernelGGL((k_gemm<1, 1>), grid, dim3(kGemmThreads), 0, st, g);
+    } else {
+        dim3 grid((N + kBN64 - 1) / kBN64, (M + kBM64 - 1) / kBM64, s.S);
+        if (!TA && !TB) hipLaunchKernelGGL((k_gemm64<0, 0>), grid, dim3(kGemmThreads), 0, st, g);
+        else if (!TA && TB) hipLaunchKernelGGL((k_gemm64<0, 1>), grid, dim3(kGemmThreads), 0, st, g);
+        else if (TA && !TB) hipLaunchKernelGGL((k_gemm64<1, 0>), grid, dim3(kGemmThreads), 0, st, g);
+        else hipLaunchKernelGGL((k_gemm64<1, 1>), grid, dim3(kGemmThreads), 0, st, g);
+    }
     if (s.S > 1) {
         const int64_t MN = (int64_t)M * N;
         hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M,

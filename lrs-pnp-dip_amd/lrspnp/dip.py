@@ -245,8 +245,10 @@ class DipConfig:
     es_size: int = 30
     patience: int = 60
     poll_every: int = 10          # host polls the device ES flag every this many steps (< es_size)
-    use_graph: bool = True
+    use_graph: bool = False       # replay one captured hipGraph per step (measured slower than
+                                  # direct launches on ROCm 7.2 for this ~110-kernel step)
     hidden: int = 128
+    early_stop: bool = True       # False: exactly num_iter steps (the timed-benchmark mode, §8d)
 
 
 class LipschitzDip:

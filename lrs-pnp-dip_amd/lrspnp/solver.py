@@ -155,7 +155,8 @@ class LrsPnP:
         """U = DIP(X + L2/mu2) (…1-LiP.py:399-411) on `stream`; the host polls early stopping."""
         ops.unfolded_to_image(self.X, self.L2, self.c2, self.H, self.W, self.dip_in, stream=stream)
         with torch.cuda.stream(stream):
-            img = self.dip.run(self.dip_target, self.dip_in, self.dip_mask, seed=self.cfg.dip_seed + self.iteration)
+            img = self.dip.run(self.dip_target, self.dip_in, self.dip_mask, seed=self.cfg.dip_seed + self.iteration,
+                               early_stop=self.dip.cfg.early_stop)
             ops.image_to_unfolded(img, self.H, self.W, self.U, stream=stream)
         self.dip_steps.append((self.dip.last_steps, self.dip.last_stop_epoch))
 
