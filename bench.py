@@ -49,9 +49,10 @@ def parse():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="pnp", choices=["pnp", "dip"],
+    ap.add_argument("--workload", default="pnp", choices=["pnp", "dip", "dip-pro"],
                     help="pnp: BASELINE configs[1] (the headline); dip: configs[2], LRS-PnP-DIP(1-Lip) on a "
-                         "196x196x198 cube (the 200x200 cube cropped to a size the U-Net maps onto itself)")
+                         "196x196x198 cube (the 200x200 cube cropped to a size the U-Net maps onto itself); "
+                         "dip-pro: configs[3], LRS-PnP-DIP with the skip net on a 512x512x224 cube")
     ap.add_argument("--dip-steps", type=int, default=100, help="DIP steps per outer iteration (ES off, §8d)")
     return ap.parse_args()
 
@@ -109,17 +110,18 @@ def cpu_baseline(Y, M, D, bb, nit, budget_s):
                       f"est. {t_iter:.1f}s per outer iteration"}
 
 
-def unet_flops_per_step(units, H, W):
-    """Algorithmic MFMA FLOPs of one DIP training step: forward convs + dW + dX (no dX of unit 0)."""
-    from lrspnp.dip import out_size
-    fwd = bwd = 0
-    h, w = H, W
-    for i, u in enumerate(units):
-        h, w = out_size(h, w, u.k, u.stride, u.pad, u.upsample)
-        f = 2 * u.cout * u.cin * u.k * u.k * h * w
-        fwd += f
-        bwd += f * (2 if i > 0 else 1)
-    return fwd + bwd
+def dip_flops_per_step(net):
+    """Algorithmic MFMA FLOPs of one DIP training step of a DipNet: conv forward + dW + dX (no dX
+    for a conv reading the network input)."""
+    sh = [net.in_shape] + list(net.shapes)
+    tot = 0
+    for i, nd in enumerate(net.nodes):
+        if nd.kind != 0:
+            continue
+        co, ho, wo = sh[i + 1]
+        f = 2 * co * sh[nd.in0][0] * nd.k * nd.k * ho * wo
+        tot += f * (2 if nd.in0 == 0 else 3)
+    return tot
 
 
 def main_dip(args):
@@ -127,15 +129,16 @@ def main_dip(args):
 
     from lrspnp import LrsPnP, LrsPnPConfig
     from lrspnp import dist as D
-    from lrspnp.dip import DipConfig, lipschitz_unet_units
+    from lrspnp.dip import DipConfig
     from lrspnp.metrics import mpsnr
     ctx = D.init_from_env("nccl")
-    H = W = 196
-    B = 198
+    pro = args.workload == "dip-pro"
+    H = W = 512 if pro else 196
+    B = 224 if pro else 198
     bb = 36 if args.bb == 8 else args.bb
     Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=ctx.rank)
-    dcfg = DipConfig(num_iter=args.dip_steps, early_stop=False)
-    cfg = LrsPnPConfig.dip_1lip(bb=bb, sliding=bb, dip=dcfg)
+    dcfg = DipConfig(num_iter=args.dip_steps, early_stop=False, net="skip" if pro else "unet1lip")
+    cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, dip=dcfg)
     s = LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
     clean_d = torch.from_numpy(clean).cuda()
     mp0 = mpsnr(s.X, clean_d)
@@ -155,17 +158,20 @@ def main_dip(args):
     elapsed = D.timed_steps(s.step, args.steps, args.warmup, ctx)
     dip_ms = float(np.mean([a.elapsed_time(b) for a, b in ev[args.warmup:]]))
     mp1 = mpsnr(s.X, clean_d)
-    flops = unet_flops_per_step(lipschitz_unet_units(B, B, 128), H, W) * args.dip_steps
+    flops = dip_flops_per_step(s.dip.net) * args.dip_steps
     achieved = flops / (dip_ms * 1e-3) / 1e12
     out = {
         "metric": METRIC, "value": ctx.world * args.steps / elapsed, "unit": "outer_iters/s",
         "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32 (MFMA) + f64 (NLM, BN/sigma statistics)",
-        "data": "synthetic (seeded low-rank 196x196x198 cube per rank, random-init U-Net per outer iteration)",
-        "config": {"workload": f"LRS-PnP-DIP(1-Lip) 196x196x198, {bb}x{bb} blocks, K={args.K}, Nit=100 fro4 ISTA, "
-                               f"DIP my_Lipschitz_Unet (198->128->198 ch) {args.dip_steps} Adam steps, ES off "
-                               "(BASELINE configs[2])", "blocks": s.nb,
+        "data": f"synthetic (seeded low-rank {H}x{W}x{B} cube per rank, random-init DIP net per outer iteration)",
+        "config": {"workload": (f"LRS-PnP-DIP(pro) {H}x{W}x{B}, {bb}x{bb} blocks, K={args.K}, Nit=100 fro4 ISTA, "
+                                f"DIP skip net (5x128 ch, 128 skips) {args.dip_steps} Adam steps, ES off "
+                                "(BASELINE configs[3])") if pro else
+                               (f"LRS-PnP-DIP(1-Lip) 196x196x198, {bb}x{bb} blocks, K={args.K}, Nit=100 fro4 ISTA, "
+                                f"DIP my_Lipschitz_Unet (198->128->198 ch) {args.dip_steps} Adam steps, ES off "
+                                "(BASELINE configs[2])"), "blocks": s.nb,
                    "parallelism": f"{ctx.world} independent cube(s), one per GPU"},
         "roofline": {"bound": "mfma", "kernel": "DIP training (conv GEMMs + BN/sigma/Adam kernels)",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -179,7 +185,7 @@ def main_dip(args):
 
 def main():
     args = parse()
-    if args.workload == "dip":
+    if args.workload in ("dip", "dip-pro"):
         return main_dip(args)
     import torch
 

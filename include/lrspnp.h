@@ -203,26 +203,38 @@ int lrs_es_init(lrs_es_state *st, int size, int patience, void *stream);
 int lrs_es_update_f32(const float *out, int64_t N, float *ring, lrs_es_state *st, void *stream);
 
 /* ---- Whole network + training step ---------------------------------------------------------
- * A sequential stack of conv units (the 1-Lip U-Net is one).  The host object holds shapes and
- * offsets only; parameters, gradients, Adam moments and the workspace are caller-owned device
- * buffers given to lrs_dipnet_bind. */
+ * A DAG of nodes; tensor 0 is the network input (C x H x W), node i produces tensor i + 1 and
+ * may read any earlier tensor.  The 1-Lip U-Net is a chain of CONV nodes; the skip net
+ * (models/skip.py) adds BN and CONCAT nodes.  The host object holds shapes and offsets only;
+ * parameters, gradients, Adam moments and the workspace are caller-owned device buffers given
+ * to lrs_dipnet_bind. */
+#define LRS_NODE_CONV 0    /* [upsample x2] -> pad -> conv(k, stride) -> [BN] -> act            */
+#define LRS_NODE_BN 1      /* BN -> act on in0                                                  */
+#define LRS_NODE_CONCAT 2  /* cat(in0, [upsample x2](in1)) along channels, centre-cropped       */
+#define LRS_BN_NONE 0
+#define LRS_BN_PLAIN 1     /* nn.BatchNorm2d, train mode (models/common.py:71)                 */
+#define LRS_BN_LIP 2       /* BatchNormSpectralNorm-wrapped (lipschitz_constraint_layer.py:88)  */
+#define LRS_WINIT_DEFAULT 0   /* nn.Conv2d default init: U(-1/sqrt(fan_in), +)                  */
+#define LRS_WINIT_KAIMING 1   /* kaiming_uniform_(a=0, fan_in) (lipschitz_constraint_layer.py:74) */
 typedef struct {
-    int32_t cin, cout, k, stride, pad, pad_mode, upsample, bn, act;
-} lrs_conv_unit;
+    int32_t kind, in0, in1, cout, k, stride, pad, pad_mode, upsample, bn, act, sn, winit;
+} lrs_dip_node;
 typedef struct lrs_dipnet lrs_dipnet;
-int lrs_dipnet_create(const lrs_conv_unit *units, int n_units, int H, int W, lrs_dipnet **out);
+int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, int H, int W, lrs_dipnet **out);
 void lrs_dipnet_destroy(lrs_dipnet *net);
 int64_t lrs_dipnet_num_params(const lrs_dipnet *net);
 int64_t lrs_dipnet_num_bnstats(const lrs_dipnet *net);
 size_t lrs_dipnet_workspace(const lrs_dipnet *net);
-/* offsets (floats) of unit i's parameters in the flat buffer; -1 when absent */
-int lrs_dipnet_param_offsets(const lrs_dipnet *net, int unit, int64_t *w, int64_t *b, int64_t *gamma,
+/* offsets (floats) of node i's parameters in the flat buffer; -1 when absent */
+int lrs_dipnet_param_offsets(const lrs_dipnet *net, int node, int64_t *w, int64_t *b, int64_t *gamma,
                              int64_t *beta);
+/* shape of node i's output (node = -1: the input) */
+int lrs_dipnet_node_shape(const lrs_dipnet *net, int node, int *C, int *H, int *W);
 int lrs_dipnet_out_shape(const lrs_dipnet *net, int *C, int *H, int *W);
 int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, float *adam_m, float *adam_v,
                     float *bnstats, void *ws, size_t ws_bytes);
-/* Kaiming-uniform(a=0, fan_in) conv weights, torch-default biases, gamma = 1, beta = 0, zero Adam
- * state; a counter-based RNG keyed by seed (the reference draws from the unseeded torch RNG). */
+/* Conv weights per node winit, torch-default biases, gamma = 1, beta = 0, zero Adam state; a
+ * counter-based RNG keyed by seed (the reference draws from the unseeded torch RNG). */
 int lrs_dipnet_init_params(lrs_dipnet *net, uint64_t seed, void *stream);
 /* zero the Adam moments and the step count (a fresh optimizer on the current parameters) */
 int lrs_dipnet_reset_optimizer(lrs_dipnet *net, void *stream);

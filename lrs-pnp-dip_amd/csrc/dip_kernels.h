@@ -46,6 +46,7 @@ struct GemmArgs {
     const float *bias;   // [M] or null (split == 1 only)
     const float *div;    // scalar divisor (device) or null (split == 1 only)
     int M, N, K, kchunk;
+    int accum;           // final C += result instead of C = result
 };
 
 // A 128(x) x 16(k) operand tile, 8 values per thread, as two float4 of 4 consecutive k.
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
                     if (final_out) {
                         if (g.bias) v = v + g.bias[m];
                         if (g.div) v = v / dv;
+                        if (g.accum) v = C[(int64_t)m * g.N + n] + v;
                     }
                     C[(int64_t)m * g.N + n] = v;
                 }
@@ -255,6 +257,7 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm64(GemmArgs g) {
                     if (final_out) {
                         if (g.bias) v = v + g.bias[m];
                         if (g.div) v = v / dv;
+                        if (g.accum) v = C[(int64_t)m * g.N + n] + v;
                     }
                     C[(int64_t)m * g.N + n] = v;
                 }
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm64(GemmArgs g) {
 // C = (sum_z part[z]) (+ bias[m]) (/ *div): fixed summation order (deterministic); 8 partial
 // chains so the loads of a long split stay in flight
 __global__ void k_gemm_reduce(const float *__restrict__ part, int nsplit, int M, int N, const float *bias,
-                              const float *div, float *__restrict__ C) {
+                              const float *div, int accum, float *__restrict__ C) {
     const int64_t MN = (int64_t)M * N;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= MN) return;
@@ -278,6 +281,7 @@ __global__ void k_gemm_reduce(const float *__restrict__ part, int nsplit, int M,
     float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     if (bias) s = s + bias[i / N];
     if (div) s = s / *div;
+    if (accum) s = C[i] + s;
     C[i] = s;
 }
 
@@ -333,7 +337,7 @@ __device__ __forceinline__ int padded_sources(int u, int n, int pad, int mode, i
 }
 
 // dx[c][y][x] = sum over every col entry that read it (adjoint of k_im2col), gather form.
-__global__ void k_col2im(const float *__restrict__ dcol, ConvGeom gm, float *__restrict__ dx) {
+__global__ void k_col2im(const float *__restrict__ dcol, ConvGeom gm, float *__restrict__ dx, int accum) {
     const int64_t total = (int64_t)gm.Cin * gm.Hs * gm.Ws;
     const int64_t P = (int64_t)gm.Ho * gm.Wo;
     const int k = gm.k, s = gm.stride;
@@ -367,7 +371,7 @@ __global__ void k_col2im(const float *__restrict__ dcol, ConvGeom gm, float *__r
                     }
             }
         }
-        dx[i] = acc;
+        dx[i] = accum ? dx[i] + acc : acc;
     }
 }
 
@@ -461,6 +465,7 @@ struct BnArgs {
     double *part;                // [C][S][3] partials
     int C, P, S, chunk, bn, act;
     float eps, momentum;
+    int lip;                     // BatchNormSpectralNorm rescale (1-Lip) or plain BatchNorm2d
 };
 
 // partial sums of (z - K), (z - K)^2 over this workgroup's slice, K = z[c][0] (stable variance)
@@ -499,7 +504,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_apply(BnArgs a) {
         for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) y[i] = act_fwd(z[i], a.act);
         return;
     }
-    const float cs = bn_lip_scale(a.gamma, a.C, redf);
+    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
     if (threadIdx.x == 0) {
         double t1 = 0.0, t2 = 0.0;
         const double *q = a.part + (int64_t)c * a.S * 3;
@@ -537,6 +542,8 @@ struct BnBwdArgs {
     float *gbias;                // [C] grad of the conv bias = sum_p dL/dz
     double *part;                // [C][S][3] partials
     int C, P, S, chunk, bn, act;
+    int lip;                     // BatchNormSpectralNorm rescale (1-Lip) or plain BatchNorm2d
+    int accum;                   // gz += instead of gz =
 };
 
 __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
@@ -586,10 +593,13 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_apply(BnBwdArgs a) {
     }
     if (!a.bn) {
         if (threadIdx.x == 0 && sb == 0 && a.gbias) a.gbias[c] = (float)t[0];
-        for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) gz[i] = act_bwd(gy[i], y[i], a.act);
+        for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+            const float v = act_bwd(gy[i], y[i], a.act);
+            gz[i] = a.accum ? gz[i] + v : v;
+        }
         return;
     }
-    const float cs = bn_lip_scale(a.gamma, a.C, redf);
+    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
     const float m32 = a.mean[c], is32 = a.invstd[c];
     const float gm = a.gamma[c] / cs;
     const float k = gm * is32;
@@ -609,7 +619,8 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_apply(BnBwdArgs a) {
     for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const float g = act_bwd(gy[i], y[i], a.act);
         const float xh = (z[i] - m32) * is32;
-        gz[i] = k * (g - mg - xh * mgx);
+        const float v = k * (g - mg - xh * mgx);
+        gz[i] = a.accum ? gz[i] + v : v;
     }
 }
 
@@ -926,6 +937,71 @@ __global__ void k_es_decide(int64_t N, lrs_es_state *st) {
         }
     }
     st->var_acc = 0.0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Concat (models/common.py:11-42): out = cat(a, up2?(b)) along channels, both centre-cropped to
+// the smaller H and W (offset (size - target) // 2, :27-37).
+// ------------------------------------------------------------------------------------------
+struct CatGeom {
+    int Ca, Ha, Wa, Cb, Hb, Wb, upb;   // b is (Cb, Hb, Wb) before the optional nearest x2
+    int H, W;                          // output spatial size
+    int oay, oax, oby, obx;            // crop offsets into a and into up2(b)
+};
+
+__global__ void k_concat_fwd(const float *__restrict__ a, const float *__restrict__ b, CatGeom g,
+                             float *__restrict__ out) {
+    const int64_t HW = (int64_t)g.H * g.W, n = (int64_t)(g.Ca + g.Cb) * HW;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i / HW);
+        const int p = (int)(i - (int64_t)c * HW);
+        const int y = p / g.W, x = p - y * g.W;
+        float v;
+        if (c < g.Ca) {
+            v = a[((int64_t)c * g.Ha + y + g.oay) * g.Wa + x + g.oax];
+        } else {
+            int yy = y + g.oby, xx = x + g.obx;
+            if (g.upb) { yy >>= 1; xx >>= 1; }
+            v = b[((int64_t)(c - g.Ca) * g.Hb + yy) * g.Wb + xx];
+        }
+        out[i] = v;
+    }
+}
+
+// ga (nullable) / gb (nullable): gather the output gradient back (zeros outside the crop;
+// the 2x2 children of an upsampled b pixel are summed); accumulate flags per input
+__global__ void k_concat_bwd(const float *__restrict__ go, CatGeom g, float *__restrict__ ga, int acc_a,
+                             float *__restrict__ gb, int acc_b) {
+    const int64_t HW = (int64_t)g.H * g.W;
+    const int64_t na = ga ? (int64_t)g.Ca * g.Ha * g.Wa : 0;
+    const int64_t nb = gb ? (int64_t)g.Cb * g.Hb * g.Wb : 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < na) {
+            const int64_t hw = (int64_t)g.Ha * g.Wa;
+            const int c = (int)(i / hw);
+            const int p = (int)(i - (int64_t)c * hw);
+            const int y = p / g.Wa - g.oay, x = p % g.Wa - g.oax;
+            float v = 0.0f;
+            if (y >= 0 && y < g.H && x >= 0 && x < g.W) v = go[(int64_t)c * HW + (int64_t)y * g.W + x];
+            ga[i] = acc_a ? ga[i] + v : v;
+        } else {
+            const int64_t j = i - na;
+            const int64_t hw = (int64_t)g.Hb * g.Wb;
+            const int c = (int)(j / hw);
+            const int p = (int)(j - (int64_t)c * hw);
+            const int Y = p / g.Wb, X = p % g.Wb;
+            const float *gc = go + (int64_t)(g.Ca + c) * HW;
+            float v = 0.0f;
+            const int f = g.upb ? 2 : 1;
+            for (int dy = 0; dy < f; ++dy)
+                for (int dx = 0; dx < f; ++dx) {
+                    const int y = Y * f + dy - g.oby, x = X * f + dx - g.obx;
+                    if (y >= 0 && y < g.H && x >= 0 && x < g.W) v += gc[(int64_t)y * g.W + x];
+                }
+            gb[j] = acc_b ? gb[j] + v : v;
+        }
+    }
 }
 
 }  // namespace lrs

@@ -83,10 +83,10 @@ int64_t gemm_part_floats(int M, int N, int K) {
 
 // C = op(A) op(B) (+ bias) (/ *div); part: split-K scratch (>= gemm_part_floats)
 int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *bias, const float *div, int M,
-         int N, int K, float *part, int64_t part_cap, hipStream_t st) {
+         int N, int K, float *part, int64_t part_cap, hipStream_t st, int accum = 0) {
     if (M <= 0 || N <= 0) return LRS_OK;
     const Split s = choose_split(M, N, K);
-    GemmArgs g{A, B, C, bias, div, M, N, K, s.kchunk};
+    GemmArgs g{A, B, C, bias, div, M, N, K, s.kchunk, accum};
     if (s.S > 1) {
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
         g.C = part;
@@ -107,7 +107,7 @@ int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *
     if (s.S > 1) {
         const int64_t MN = (int64_t)M * N;
         hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M,
-                           N, bias, div, C);
+                           N, bias, div, accum, C);
     }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
@@ -138,16 +138,16 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
 
 // gw = gz col^T / div ; gx = col2im(w^T gz) (gx nullable).  dcol: Kc*P floats when !plain.
 int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *w, const float *div, int Cout,
-             float *gx, float *gw, float *dcol, float *part, int64_t part_cap, hipStream_t st) {
+             float *gx, float *gw, float *dcol, float *part, int64_t part_cap, hipStream_t st, int accum_gx = 0) {
     const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
     int rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
     if (rc || !gx) return rc;
-    if (plain_unit(g)) return gemm(1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st);
+    if (plain_unit(g)) return gemm(1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st, accum_gx);
     if (!dcol) return LRS_E_WORKSPACE;
     rc = gemm(1, 0, w, gz, dcol, nullptr, nullptr, Kc, P, Cout, part, part_cap, st);
     if (rc) return rc;
     const int64_t n = (int64_t)g.Cin * g.Hs * g.Ws;
-    hipLaunchKernelGGL(k_col2im, dim3(ew_blocks(n, 1 << 16)), dim3(kEw), 0, st, dcol, g, gx);
+    hipLaunchKernelGGL(k_col2im, dim3(ew_blocks(n, 1 << 16)), dim3(kEw), 0, st, dcol, g, gx, accum_gx);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -163,10 +163,10 @@ inline int bn_split(int64_t P) {
 inline int64_t bn_part_doubles(int C, int64_t P) { return (int64_t)C * bn_split(P) * 3; }
 
 int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, float *mean, float *invstd, float *rm,
-           float *rv, int C, int64_t P, int act, float eps, float mom, double *part, hipStream_t st) {
+           float *rv, int C, int64_t P, int act, float eps, float mom, double *part, hipStream_t st, int lip = 1) {
     const int S = bn_split(P);
     const int chunk = (int)((P + S - 1) / S);
-    BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, part, C, (int)P, S, chunk, gamma ? 1 : 0, act, eps, mom};
+    BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, part, C, (int)P, S, chunk, gamma ? 1 : 0, act, eps, mom, lip};
     if (gamma) hipLaunchKernelGGL(k_bn_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
     hipLaunchKernelGGL(k_bn_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
     LRS_CHECK_LAUNCH();
@@ -175,11 +175,11 @@ int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, floa
 
 int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, const float *mean,
            const float *invstd, float *gz, float *ggamma, float *gbeta, float *gbias, int C, int64_t P, int act,
-           double *part, hipStream_t st) {
+           double *part, hipStream_t st, int lip = 1, int accum = 0) {
     const int S = bn_split(P);
     const int chunk = (int)((P + S - 1) / S);
     BnBwdArgs a{gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, part, C, (int)P, S, chunk,
-                gamma ? 1 : 0, act};
+                gamma ? 1 : 0, act, lip, accum};
     if (gamma || gbias) hipLaunchKernelGGL(k_bn_bwd_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
     hipLaunchKernelGGL(k_bn_bwd_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
     LRS_CHECK_LAUNCH();
@@ -452,30 +452,30 @@ extern "C" int lrs_es_update_f32(const float *out, int64_t N, float *ring, lrs_e
 }
 
 // ============================================================================================
-// Sequential network engine
+// Network engine: a DAG of conv / BN / concat nodes (the 1-Lip U-Net is a chain; the skip net
+// of models/skip.py has concatenations).  Tensor 0 is the input, node i produces tensor i+1.
 // ============================================================================================
 struct lrs_dipnet {
-    struct Unit {
-        lrs_conv_unit u;
-        ConvGeom g;
-        int64_t P, Kc;
-        int64_t w_off, b_off, gm_off, bt_off, rs_off;   // params / bn running stats
-        int64_t act_off, z_off, col_off, mean_off, istd_off, wn_off;   // workspace (floats)
+    struct Node {
+        lrs_dip_node d;
+        int C, H, W;                  // output shape
+        ConvGeom g{};                 // CONV
+        CatGeom cg{};                 // CONCAT
+        int64_t P = 0, Kc = 0;
+        int64_t w_off = -1, b_off = -1, gm_off = -1, bt_off = -1, rs_off = -1;   // params / bn running stats
+        int64_t out_off = 0, z_off = -1, col_off = -1, mean_off = -1, istd_off = -1, wn_off = -1, grad_off = 0;
+        int sn_index = -1;            // position in the spectral-norm table
     };
-    std::vector<Unit> units;
-    int H = 0, W = 0;
+    std::vector<Node> nodes;
+    int C0 = 0, H = 0, W = 0;
     int64_t n_params = 0, n_bnstats = 0;
-    // workspace layout (floats unless noted)
-    int64_t ws_floats = 0;
-    int64_t ga_off = 0, gb_off = 0, dz_off = 0, dcol_off = 0, part_off = 0, part_cap = 0;
-    int64_t sigma_off = 0, scale_off = 0, gram_off_bytes = 0, table_off_bytes = 0, misc_off_bytes = 0;
-    int64_t bnpart_off_bytes = 0, ticket_off_bytes = 0, ticket_bytes = 0;
+    int64_t dz_off = 0, dcol_off = 0, part_off = 0, part_cap = 0, sigma_off = 0, scale_off = 0;
+    int64_t gram_off_bytes = 0, table_off_bytes = 0, misc_off_bytes = 0, bnpart_off_bytes = 0;
     size_t ws_bytes = 0;
+    int n_sn = 0;
     int64_t max_w = 0;
-    // bound buffers
     float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr, *bnstats = nullptr;
     char *ws = nullptr;
-    // graph cache
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
     struct Key {
@@ -490,7 +490,10 @@ struct lrs_dipnet {
     double *loss_acc() const { return (double *)(ws + misc_off_bytes); }
     int *step() const { return (int *)(ws + misc_off_bytes + 8); }
     double *bnpart() const { return (double *)(ws + bnpart_off_bytes); }
-    int *ticket() const { return (int *)(ws + ticket_off_bytes); }
+    const float *tensor(int t, const float *x) const { return t == 0 ? x : f(nodes[t - 1].out_off); }
+    int tC(int t) const { return t == 0 ? C0 : nodes[t - 1].C; }
+    int tH(int t) const { return t == 0 ? H : nodes[t - 1].H; }
+    int tW(int t) const { return t == 0 ? W : nodes[t - 1].W; }
 };
 
 namespace {
@@ -498,26 +501,40 @@ namespace {
 int64_t align64(int64_t n) { return (n + 63) / 64 * 64; }   // floats (256 bytes)
 
 int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
-    const int n = (int)net->units.size();
-    int rc = sn_launch(net->table(), n, net->max_w, net->gram(), net->f(net->sigma_off), net->f(net->scale_off), 1.0f,
-                       true, st);
-    if (rc) return rc;
-    const float *src = x;
-    for (int i = 0; i < n; ++i) {
-        auto &U = net->units[i];
-        const bool bn = U.u.bn != 0;
-        float *act = net->f(U.act_off);
-        float *z = bn ? net->f(U.z_off) : act;
-        rc = conv_fwd(U.g, src, net->f(U.wn_off), net->params + U.b_off, U.u.cout,
-                      U.col_off >= 0 ? net->f(U.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st);
+    int rc;
+    if (net->n_sn) {
+        rc = sn_launch(net->table(), net->n_sn, net->max_w, net->gram(), net->f(net->sigma_off),
+                       net->f(net->scale_off), 1.0f, true, st);
         if (rc) return rc;
-        rc = bn_fwd(z, act, bn ? net->params + U.gm_off : nullptr, bn ? net->params + U.bt_off : nullptr,
-                    net->f(U.mean_off), net->f(U.istd_off), bn ? net->bnstats + U.rs_off : nullptr,
-                    bn ? net->bnstats + U.rs_off + U.u.cout : nullptr, U.u.cout, U.P, U.u.act, 1e-5f, 0.1f,
-                    net->bnpart(), st);
-        if (rc) return rc;
-        src = act;
     }
+    for (size_t i = 0; i < net->nodes.size(); ++i) {
+        auto &N = net->nodes[i];
+        float *out = net->f(N.out_off);
+        const int lip = N.d.bn == 2 ? 1 : 0;
+        if (N.d.kind == LRS_NODE_CONV) {
+            const bool bn = N.d.bn != 0;
+            float *z = bn ? net->f(N.z_off) : out;
+            const float *w = N.sn_index >= 0 ? net->f(N.wn_off) : net->params + N.w_off;
+            rc = conv_fwd(N.g, net->tensor(N.d.in0, x), w, net->params + N.b_off, N.C,
+                          N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st);
+            if (rc) return rc;
+            rc = bn_fwd(z, out, bn ? net->params + N.gm_off : nullptr, bn ? net->params + N.bt_off : nullptr,
+                        net->f(N.mean_off), net->f(N.istd_off), bn ? net->bnstats + N.rs_off : nullptr,
+                        bn ? net->bnstats + N.rs_off + N.C : nullptr, N.C, N.P, N.d.act, 1e-5f, 0.1f, net->bnpart(), st,
+                        lip);
+        } else if (N.d.kind == LRS_NODE_BN) {
+            rc = bn_fwd(net->tensor(N.d.in0, x), out, net->params + N.gm_off, net->params + N.bt_off,
+                        net->f(N.mean_off), net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C,
+                        N.C, N.P, N.d.act, 1e-5f, 0.1f, net->bnpart(), st, lip);
+        } else {
+            const int64_t n = (int64_t)N.C * N.P;
+            hipLaunchKernelGGL(k_concat_fwd, dim3(ew_blocks(n, 1 << 16)), dim3(kEw), 0, st, net->tensor(N.d.in0, x),
+                               net->tensor(N.d.in1, x), N.cg, out);
+            rc = LRS_OK;
+        }
+        if (rc) return rc;
+    }
+    LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
 
@@ -525,39 +542,82 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
                 float eps, lrs_es_state *es, float *ring, hipStream_t st) {
     int rc = dipnet_forward(net, x, st);
     if (rc) return rc;
-    const int n = (int)net->units.size();
-    const auto &L = net->units[n - 1];
-    const float *out = net->f(L.act_off);
-    const int64_t Pout = L.P;
+    const int n = (int)net->nodes.size();
+    const auto &Lst = net->nodes[n - 1];
+    const float *out = net->f(Lst.out_off);
     hipError_t e = hipMemsetAsync(net->loss_acc(), 0, sizeof(double), st);
     if (e != hipSuccess) return (int)e;
-    float *g = net->f(net->ga_off), *g2 = net->f(net->gb_off);
-    rc = lrs_masked_mse_f32(out, target, mask, L.u.cout, Pout, g, net->loss_acc(), st);
+    rc = lrs_masked_mse_f32(out, target, mask, Lst.C, Lst.P, net->f(Lst.grad_off), net->loss_acc(), st);
     if (rc) return rc;
+    // gradient buffers: the first contribution to a tensor writes, later ones accumulate
+    std::vector<char> written(n + 1, 0);
+    written[n] = 1;
     for (int i = n - 1; i >= 0; --i) {
-        auto &U = net->units[i];
-        const bool bn = U.u.bn != 0;
-        float *act = net->f(U.act_off);
-        float *z = bn ? net->f(U.z_off) : act;
-        float *gz = net->f(net->dz_off);
-        rc = bn_bwd(g, act, z, bn ? net->params + U.gm_off : nullptr, net->f(U.mean_off), net->f(U.istd_off), gz,
-                    bn ? net->grads + U.gm_off : nullptr, bn ? net->grads + U.bt_off : nullptr, net->grads + U.b_off,
-                    U.u.cout, U.P, U.u.act, net->bnpart(), st);
-        if (rc) return rc;
-        const float *colsrc = U.col_off >= 0 ? net->f(U.col_off) : (i == 0 ? x : net->f(net->units[i - 1].act_off));
-        rc = conv_bwd(U.g, gz, colsrc, net->f(U.wn_off), net->f(net->scale_off) + i, U.u.cout, i > 0 ? g2 : nullptr,
-                      net->grads + U.w_off, U.col_off >= 0 ? net->f(net->dcol_off) : nullptr, net->f(net->part_off),
-                      net->part_cap, st);
-        if (rc) return rc;
-        float *tmp = g;
-        g = g2;
-        g2 = tmp;
+        auto &N = net->nodes[i];
+        float *gout = net->f(N.grad_off);
+        float *outp = net->f(N.out_off);
+        const int lip = N.d.bn == 2 ? 1 : 0;
+        if (!written[i + 1]) continue;   // output unused by the loss (cannot happen for a valid net)
+        if (N.d.kind == LRS_NODE_CONV) {
+            const bool bn = N.d.bn != 0;
+            float *z = bn ? net->f(N.z_off) : outp;
+            float *gz = net->f(net->dz_off);
+            rc = bn_bwd(gout, outp, z, bn ? net->params + N.gm_off : nullptr, net->f(N.mean_off), net->f(N.istd_off),
+                        gz, bn ? net->grads + N.gm_off : nullptr, bn ? net->grads + N.bt_off : nullptr,
+                        net->grads + N.b_off, N.C, N.P, N.d.act, net->bnpart(), st, lip, 0);
+            if (rc) return rc;
+            const int t = N.d.in0;
+            const float *colsrc = N.col_off >= 0 ? net->f(N.col_off) : net->tensor(t, x);
+            const bool sn = N.sn_index >= 0;
+            const float *w = sn ? net->f(N.wn_off) : net->params + N.w_off;
+            float *gx = t > 0 ? net->f(net->nodes[t - 1].grad_off) : nullptr;
+            rc = conv_bwd(N.g, gz, colsrc, w, sn ? net->f(net->scale_off) + N.sn_index : nullptr, N.C, gx,
+                          net->grads + N.w_off, N.col_off >= 0 ? net->f(net->dcol_off) : nullptr,
+                          net->f(net->part_off), net->part_cap, st, t > 0 ? written[t] : 0);
+            if (rc) return rc;
+            if (t > 0) written[t] = 1;
+        } else if (N.d.kind == LRS_NODE_BN) {
+            const int t = N.d.in0;
+            if (t > 0) {
+                rc = bn_bwd(gout, outp, net->tensor(t, x), net->params + N.gm_off, net->f(N.mean_off),
+                            net->f(N.istd_off), net->f(net->nodes[t - 1].grad_off), net->grads + N.gm_off,
+                            net->grads + N.bt_off, nullptr, N.C, N.P, N.d.act, net->bnpart(), st, lip, written[t]);
+                written[t] = 1;
+            } else {   // BN straight on the input: parameter grads only
+                rc = bn_bwd(gout, outp, net->tensor(t, x), net->params + N.gm_off, net->f(N.mean_off),
+                            net->f(N.istd_off), net->f(net->dz_off), net->grads + N.gm_off, net->grads + N.bt_off,
+                            nullptr, N.C, N.P, N.d.act, net->bnpart(), st, lip, 0);
+            }
+            if (rc) return rc;
+        } else {
+            const int ta = N.d.in0, tb = N.d.in1;
+            float *ga = ta > 0 ? net->f(net->nodes[ta - 1].grad_off) : nullptr;
+            float *gb = tb > 0 ? net->f(net->nodes[tb - 1].grad_off) : nullptr;
+            const int64_t na = ga ? (int64_t)N.cg.Ca * N.cg.Ha * N.cg.Wa : 0;
+            const int64_t nb = gb ? (int64_t)N.cg.Cb * N.cg.Hb * N.cg.Wb : 0;
+            if (na + nb > 0) {
+                const int acc_a = ta > 0 ? written[ta] : 0;
+                // both inputs may be the same tensor: the b pass must then accumulate onto the a pass
+                const int acc_b = tb > 0 ? (written[tb] || (tb == ta)) : 0;
+                if (ta == tb && ga) {
+                    hipLaunchKernelGGL(k_concat_bwd, dim3(ew_blocks(na, 1 << 16)), dim3(kEw), 0, st, gout, N.cg, ga,
+                                       acc_a, nullptr, 0);
+                    hipLaunchKernelGGL(k_concat_bwd, dim3(ew_blocks(nb, 1 << 16)), dim3(kEw), 0, st, gout, N.cg,
+                                       nullptr, 0, gb, 1);
+                } else {
+                    hipLaunchKernelGGL(k_concat_bwd, dim3(ew_blocks(na + nb, 1 << 16)), dim3(kEw), 0, st, gout, N.cg,
+                                       ga, acc_a, gb, acc_b);
+                }
+            }
+            if (ta > 0) written[ta] = 1;
+            if (tb > 0) written[tb] = 1;
+        }
     }
     hipLaunchKernelGGL(k_counter_inc, dim3(1), dim3(64), 0, st, net->step());
     rc = lrs_adam_f32(net->params, net->grads, net->am, net->av, net->n_params, net->step(), lr, b1, b2, eps, st);
     if (rc) return rc;
     if (es) {
-        rc = es_update(out, (int64_t)L.u.cout * Pout, ring, es, st);
+        rc = es_update(out, (int64_t)Lst.C * Lst.P, ring, es, st);
         if (rc) return rc;
     }
     LRS_CHECK_LAUNCH();
@@ -574,79 +634,106 @@ void drop_graph(lrs_dipnet *net) {
 
 }  // namespace
 
-extern "C" int lrs_dipnet_create(const lrs_conv_unit *units, int n_units, int H, int W, lrs_dipnet **out) {
-    if (!units || n_units <= 0 || H <= 0 || W <= 0 || !out) return LRS_E_INVALID;
+extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, int H, int W, lrs_dipnet **out) {
+    if (!nodes || n_nodes <= 0 || C <= 0 || H <= 0 || W <= 0 || !out) return LRS_E_INVALID;
     lrs_dipnet *net = new (std::nothrow) lrs_dipnet();
     if (!net) return LRS_E_INVALID;
+    net->C0 = C;
     net->H = H;
     net->W = W;
-    int cin = units[0].cin, h = H, w = W;
-    int64_t pofs = 0, rofs = 0, ofs = 0, max_act = (int64_t)cin * H * W, max_dz = 0, max_dcol = 0, part = 0;
-    int64_t max_bnpart = 0, max_c = 0;
-    for (int i = 0; i < n_units; ++i) {
-        lrs_dipnet::Unit U{};
-        U.u = units[i];
-        if (U.u.cin != cin || U.u.cout <= 0) { delete net; return LRS_E_INVALID; }
-        if (U.u.act != LRS_ACT_NONE && U.u.act != LRS_ACT_LRELU && U.u.act != LRS_ACT_SIGMOID) { delete net; return LRS_E_INVALID; }
-        int rc = make_geom(cin, h, w, U.u.k, U.u.stride, U.u.pad, U.u.pad_mode, U.u.upsample, U.g);
-        if (rc) { delete net; return rc; }
-        U.P = (int64_t)U.g.Ho * U.g.Wo;
-        U.Kc = (int64_t)cin * U.u.k * U.u.k;
-        if ((U.Kc < U.u.cout ? U.Kc : U.u.cout) > kSnMaxDim) { delete net; return LRS_E_UNSUPPORTED; }
-        // parameters (flat): W_bar, bias, [gamma_orig, beta_orig]
-        U.w_off = pofs; pofs += U.u.cout * U.Kc;
-        U.b_off = pofs; pofs += U.u.cout;
-        U.gm_off = U.bt_off = U.rs_off = -1;
-        if (U.u.bn) {
-            U.gm_off = pofs; pofs += U.u.cout;
-            U.bt_off = pofs; pofs += U.u.cout;
-            U.rs_off = rofs; rofs += 2 * U.u.cout;
+    auto fail = [&](int rc) { delete net; return rc; };
+    int64_t pofs = 0, rofs = 0, ofs = 0, max_dz = 0, max_dcol = 0, part = 0, max_bnpart = 0;
+    int n_sn = 0;
+    for (int i = 0; i < n_nodes; ++i) {
+        lrs_dipnet::Node N;
+        N.d = nodes[i];
+        const int t0 = N.d.in0;
+        if (t0 < 0 || t0 > i) return fail(LRS_E_INVALID);
+        if (N.d.act != LRS_ACT_NONE && N.d.act != LRS_ACT_LRELU && N.d.act != LRS_ACT_SIGMOID) return fail(LRS_E_INVALID);
+        if (N.d.bn < 0 || N.d.bn > 2) return fail(LRS_E_INVALID);
+        const int ci = net->tC(t0), hi = net->tH(t0), wi = net->tW(t0);
+        if (N.d.kind == LRS_NODE_CONV) {
+            if (N.d.cout <= 0) return fail(LRS_E_INVALID);
+            int rc = make_geom(ci, hi, wi, N.d.k, N.d.stride, N.d.pad, N.d.pad_mode, N.d.upsample, N.g);
+            if (rc) return fail(rc);
+            N.C = N.d.cout;
+            N.H = N.g.Ho;
+            N.W = N.g.Wo;
+            N.P = (int64_t)N.H * N.W;
+            N.Kc = (int64_t)ci * N.d.k * N.d.k;
+            N.w_off = pofs; pofs += N.C * N.Kc;
+            N.b_off = pofs; pofs += N.C;
+            if (N.d.sn) {
+                if ((N.Kc < N.C ? N.Kc : N.C) > kSnMaxDim) return fail(LRS_E_UNSUPPORTED);
+                N.sn_index = n_sn++;
+                N.wn_off = ofs; ofs += align64(N.C * N.Kc);
+                if (N.C * N.Kc > net->max_w) net->max_w = N.C * N.Kc;
+            }
+            if (!plain_unit(N.g)) {
+                N.col_off = ofs; ofs += align64(N.Kc * N.P);
+                if (N.Kc * N.P > max_dcol) max_dcol = N.Kc * N.P;
+            }
+            if (N.d.bn) { N.z_off = ofs; ofs += align64(N.C * N.P); }
+            const int64_t pc = conv_part_floats(N.g, N.C);
+            if (pc > part) part = pc;
+            if (N.C * N.P > max_dz) max_dz = N.C * N.P;
+        } else if (N.d.kind == LRS_NODE_BN) {
+            if (!N.d.bn) N.d.bn = 1;
+            N.C = ci;
+            N.H = hi;
+            N.W = wi;
+            N.P = (int64_t)hi * wi;
+            if (N.C * N.P > max_dz) max_dz = N.C * N.P;
+        } else if (N.d.kind == LRS_NODE_CONCAT) {
+            const int t1 = N.d.in1;
+            if (t1 < 0 || t1 > i) return fail(LRS_E_INVALID);
+            auto &cg = N.cg;
+            cg.Ca = ci; cg.Ha = hi; cg.Wa = wi;
+            cg.Cb = net->tC(t1); cg.Hb = net->tH(t1); cg.Wb = net->tW(t1); cg.upb = N.d.upsample ? 1 : 0;
+            const int hb = cg.upb ? 2 * cg.Hb : cg.Hb, wb = cg.upb ? 2 * cg.Wb : cg.Wb;
+            cg.H = hi < hb ? hi : hb;
+            cg.W = wi < wb ? wi : wb;
+            cg.oay = (hi - cg.H) / 2; cg.oax = (wi - cg.W) / 2;
+            cg.oby = (hb - cg.H) / 2; cg.obx = (wb - cg.W) / 2;
+            N.C = cg.Ca + cg.Cb;
+            N.H = cg.H;
+            N.W = cg.W;
+            N.P = (int64_t)N.H * N.W;
+            N.d.bn = 0;
+        } else {
+            return fail(LRS_E_INVALID);
         }
-        // workspace
-        U.act_off = ofs; ofs += align64(U.u.cout * U.P);
-        U.z_off = -1;
-        if (U.u.bn) { U.z_off = ofs; ofs += align64(U.u.cout * U.P); }
-        U.col_off = -1;
-        if (!plain_unit(U.g)) {
-            U.col_off = ofs; ofs += align64(U.Kc * U.P);
-            if (i > 0 && U.Kc * U.P > max_dcol) max_dcol = U.Kc * U.P;
+        if (N.d.bn) {
+            N.gm_off = pofs; pofs += N.C;
+            N.bt_off = pofs; pofs += N.C;
+            N.rs_off = rofs; rofs += 2 * N.C;
+            N.mean_off = ofs; ofs += align64(N.C);
+            N.istd_off = ofs; ofs += align64(N.C);
+            if (bn_part_doubles(N.C, N.P) > max_bnpart) max_bnpart = bn_part_doubles(N.C, N.P);
+        } else if (N.d.kind == LRS_NODE_CONV) {
+            N.mean_off = ofs; ofs += align64(N.C);   // unused placeholders (the kernels take them)
+            N.istd_off = ofs; ofs += align64(N.C);
         }
-        U.mean_off = ofs; ofs += align64(U.u.cout);
-        U.istd_off = ofs; ofs += align64(U.u.cout);
-        U.wn_off = ofs; ofs += align64(U.u.cout * U.Kc);
-        if (U.u.cout * U.Kc > net->max_w) net->max_w = U.u.cout * U.Kc;
-        if (U.u.cout * U.P > max_act) max_act = U.u.cout * U.P;
-        if (U.u.cout * U.P > max_dz) max_dz = U.u.cout * U.P;
-        if (bn_part_doubles(U.u.cout, U.P) > max_bnpart) max_bnpart = bn_part_doubles(U.u.cout, U.P);
-        if (U.u.cout > max_c) max_c = U.u.cout;
-        const int64_t pc = conv_part_floats(U.g, U.u.cout);
-        if (pc > part) part = pc;
-        net->units.push_back(U);
-        cin = U.u.cout;
-        h = U.g.Ho;
-        w = U.g.Wo;
+        N.out_off = ofs; ofs += align64((int64_t)N.C * N.P);
+        N.grad_off = ofs; ofs += align64((int64_t)N.C * N.P);
+        net->nodes.push_back(N);
     }
+    net->n_sn = n_sn;
     net->n_params = pofs;
     net->n_bnstats = rofs;
-    net->ga_off = ofs; ofs += align64(max_act);
-    net->gb_off = ofs; ofs += align64(max_act);
     net->dz_off = ofs; ofs += align64(max_dz);
     net->dcol_off = ofs; ofs += align64(max_dcol);
     net->part_off = ofs; ofs += align64(part);
     net->part_cap = part;
-    net->sigma_off = ofs; ofs += align64(n_units);
-    net->scale_off = ofs; ofs += align64(n_units);
-    net->ws_floats = ofs;
+    net->sigma_off = ofs; ofs += align64(n_sn > 0 ? n_sn : 1);
+    net->scale_off = ofs; ofs += align64(n_sn > 0 ? n_sn : 1);
     size_t bytes = (size_t)ofs * sizeof(float);
     net->gram_off_bytes = (int64_t)bytes;
-    bytes += (size_t)n_units * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double);
+    bytes += (size_t)n_sn * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double);
     net->bnpart_off_bytes = (int64_t)bytes;
-    bytes += (size_t)round_up(max_bnpart * (int64_t)sizeof(double), 256);
-    net->ticket_off_bytes = (int64_t)bytes;
-    net->ticket_bytes = round_up(max_c * (int64_t)sizeof(int), 256);
-    bytes += (size_t)net->ticket_bytes;
+    bytes += (size_t)round_up((max_bnpart > 0 ? max_bnpart : 1) * (int64_t)sizeof(double), 256);
     net->table_off_bytes = (int64_t)bytes;
-    bytes += (size_t)round_up((int64_t)(n_units * sizeof(SnConv)), 256);
+    bytes += (size_t)round_up((int64_t)((n_sn > 0 ? n_sn : 1) * sizeof(SnConv)), 256);
     net->misc_off_bytes = (int64_t)bytes;
     bytes += 256;
     net->ws_bytes = bytes;
@@ -664,24 +751,29 @@ extern "C" int64_t lrs_dipnet_num_params(const lrs_dipnet *net) { return net ? n
 extern "C" int64_t lrs_dipnet_num_bnstats(const lrs_dipnet *net) { return net ? net->n_bnstats : -1; }
 extern "C" size_t lrs_dipnet_workspace(const lrs_dipnet *net) { return net ? net->ws_bytes : 0; }
 
-extern "C" int lrs_dipnet_param_offsets(const lrs_dipnet *net, int unit, int64_t *w, int64_t *b, int64_t *gamma,
+extern "C" int lrs_dipnet_param_offsets(const lrs_dipnet *net, int node, int64_t *w, int64_t *b, int64_t *gamma,
                                         int64_t *beta) {
-    if (!net || unit < 0 || unit >= (int)net->units.size()) return LRS_E_INVALID;
-    const auto &U = net->units[unit];
-    if (w) *w = U.w_off;
-    if (b) *b = U.b_off;
-    if (gamma) *gamma = U.gm_off;
-    if (beta) *beta = U.bt_off;
+    if (!net || node < 0 || node >= (int)net->nodes.size()) return LRS_E_INVALID;
+    const auto &N = net->nodes[node];
+    if (w) *w = N.w_off;
+    if (b) *b = N.b_off;
+    if (gamma) *gamma = N.gm_off;
+    if (beta) *beta = N.bt_off;
+    return LRS_OK;
+}
+
+extern "C" int lrs_dipnet_node_shape(const lrs_dipnet *net, int node, int *C, int *H, int *W) {
+    if (!net || node < -1 || node >= (int)net->nodes.size()) return LRS_E_INVALID;
+    const int t = node + 1;
+    if (C) *C = net->tC(t);
+    if (H) *H = net->tH(t);
+    if (W) *W = net->tW(t);
     return LRS_OK;
 }
 
 extern "C" int lrs_dipnet_out_shape(const lrs_dipnet *net, int *C, int *H, int *W) {
     if (!net) return LRS_E_INVALID;
-    const auto &L = net->units.back();
-    if (C) *C = L.u.cout;
-    if (H) *H = L.g.Ho;
-    if (W) *W = L.g.Wo;
-    return LRS_OK;
+    return lrs_dipnet_node_shape(net, (int)net->nodes.size() - 1, C, H, W);
 }
 
 extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, float *adam_m, float *adam_v,
@@ -695,37 +787,36 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
     net->av = adam_v;
     net->bnstats = bnstats;
     net->ws = (char *)ws;
-    const int n = (int)net->units.size();
-    std::vector<SnConv> tab(n);
-    for (int i = 0; i < n; ++i) {
-        const auto &U = net->units[i];
-        tab[i] = SnConv{params + U.w_off, net->f(U.wn_off), U.u.cout, (int)U.Kc};
-    }
-    hipError_t e = hipMemcpy(net->table(), tab.data(), sizeof(SnConv) * n, hipMemcpyHostToDevice);
-    if (e != hipSuccess) return (int)e;
-    e = hipMemset(net->misc_off_bytes + net->ws, 0, 256);
-    if (e == hipSuccess) e = hipMemset(net->ticket(), 0, (size_t)net->ticket_bytes);
+    std::vector<SnConv> tab;
+    for (const auto &N : net->nodes)
+        if (N.sn_index >= 0) tab.push_back(SnConv{params + N.w_off, net->f(N.wn_off), N.C, (int)N.Kc});
+    hipError_t e = hipSuccess;
+    if (!tab.empty()) e = hipMemcpy(net->table(), tab.data(), sizeof(SnConv) * tab.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(net->misc_off_bytes + net->ws, 0, 256);
     return e == hipSuccess ? LRS_OK : (int)e;
 }
 
 extern "C" int lrs_dipnet_init_params(lrs_dipnet *net, uint64_t seed, void *stream) {
     if (!net || !net->params) return LRS_E_INVALID;
     hipStream_t st = (hipStream_t)stream;
-    for (size_t i = 0; i < net->units.size(); ++i) {
-        const auto &U = net->units[i];
-        const float fan_in = (float)U.Kc;
-        const float wb = sqrtf(6.0f / fan_in);          // kaiming_uniform_(a=0, mode='fan_in'), gain sqrt(2)
-        const float bb = 1.0f / sqrtf(fan_in);          // nn.Conv2d default bias init
+    for (size_t i = 0; i < net->nodes.size(); ++i) {
+        const auto &N = net->nodes[i];
         const uint64_t k1 = mix64(seed * 0x100000001b3ULL + 2 * i + 1), k2 = mix64(seed * 0x100000001b3ULL + 2 * i + 2);
-        hipLaunchKernelGGL(k_init_uniform, dim3(ew_blocks(U.u.cout * U.Kc)), dim3(kEw), 0, st, net->params + U.w_off,
-                           (int64_t)(U.u.cout * U.Kc), wb, k1);
-        hipLaunchKernelGGL(k_init_uniform, dim3(1), dim3(kEw), 0, st, net->params + U.b_off, (int64_t)U.u.cout, bb, k2);
-        if (U.u.bn) {
-            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kEw), 0, st, net->params + U.gm_off, (int64_t)U.u.cout, 1.0f);
-            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kEw), 0, st, net->params + U.bt_off, (int64_t)U.u.cout, 0.0f);
-            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kEw), 0, st, net->bnstats + U.rs_off, (int64_t)U.u.cout, 0.0f);
-            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kEw), 0, st, net->bnstats + U.rs_off + U.u.cout,
-                               (int64_t)U.u.cout, 1.0f);
+        if (N.d.kind == LRS_NODE_CONV) {
+            const float fan_in = (float)N.Kc;
+            // kaiming_uniform_(a=0, fan_in) (lipschitz_constraint_layer.py:74) or the nn.Conv2d
+            // default kaiming_uniform_(a=sqrt(5)) = U(-1/sqrt(fan_in), +)
+            const float wb = N.d.winit == LRS_WINIT_KAIMING ? sqrtf(6.0f / fan_in) : 1.0f / sqrtf(fan_in);
+            const float bb = 1.0f / sqrtf(fan_in);
+            hipLaunchKernelGGL(k_init_uniform, dim3(ew_blocks(N.C * N.Kc)), dim3(kEw), 0, st, net->params + N.w_off,
+                               (int64_t)(N.C * N.Kc), wb, k1);
+            hipLaunchKernelGGL(k_init_uniform, dim3(1), dim3(kEw), 0, st, net->params + N.b_off, (int64_t)N.C, bb, k2);
+        }
+        if (N.d.bn) {
+            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kEw), 0, st, net->params + N.gm_off, (int64_t)N.C, 1.0f);
+            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kEw), 0, st, net->params + N.bt_off, (int64_t)N.C, 0.0f);
+            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kEw), 0, st, net->bnstats + N.rs_off, (int64_t)N.C, 0.0f);
+            hipLaunchKernelGGL(k_fill, dim3(1), dim3(kEw), 0, st, net->bnstats + N.rs_off + N.C, (int64_t)N.C, 1.0f);
         }
     }
     hipError_t e = hipMemsetAsync(net->am, 0, sizeof(float) * net->n_params, st);
@@ -752,7 +843,7 @@ extern "C" int lrs_dipnet_forward(lrs_dipnet *net, const float *x, void *stream)
 }
 
 extern "C" const float *lrs_dipnet_output(const lrs_dipnet *net) {
-    return (net && net->ws) ? net->f(net->units.back().act_off) : nullptr;
+    return (net && net->ws) ? net->f(net->nodes.back().out_off) : nullptr;
 }
 
 extern "C" const float *lrs_dipnet_grads(const lrs_dipnet *net) { return net ? net->grads : nullptr; }
@@ -805,7 +896,7 @@ extern "C" int lrs_dipnet_last_loss(lrs_dipnet *net, double *loss, void *stream)
     hipError_t e = hipMemcpyAsync(&acc, net->loss_acc(), sizeof(double), hipMemcpyDeviceToHost, (hipStream_t)stream);
     if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
     if (e != hipSuccess) return (int)e;
-    const auto &L = net->units.back();
-    *loss = acc / ((double)L.u.cout * (double)L.P);
+    const auto &L = net->nodes.back();
+    *loss = acc / ((double)L.C * (double)L.P);
     return LRS_OK;
 }

@@ -79,7 +79,8 @@ def _declare(L):
         "lrs_image_to_unfolded_f32": (i32, [vp, i64, i64, i64, vp, vp]),
         "lrs_es_init": (i32, [vp, i32, i32, vp]),
         "lrs_es_update_f32": (i32, [vp, i64, vp, vp, vp]),
-        "lrs_dipnet_create": (i32, [vp, i32, i32, i32, c.POINTER(vp)]),
+        "lrs_dipnet_create": (i32, [vp, i32, i32, i32, i32, c.POINTER(vp)]),
+        "lrs_dipnet_node_shape": (i32, [vp, i32, c.POINTER(c.c_int), c.POINTER(c.c_int), c.POINTER(c.c_int)]),
         "lrs_dipnet_destroy": (None, [vp]),
         "lrs_dipnet_num_params": (i64, [vp]),
         "lrs_dipnet_num_bnstats": (i64, [vp]),

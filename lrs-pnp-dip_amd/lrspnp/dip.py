@@ -26,15 +26,25 @@ from . import _lib
 
 PAD_ZERO, PAD_REFLECT = 0, 1
 ACT_NONE, ACT_LRELU, ACT_SIGMOID = 0, 1, 2
+NODE_CONV, NODE_BN, NODE_CONCAT = 0, 1, 2
+BN_NONE, BN_PLAIN, BN_LIP = 0, 1, 2
+WINIT_DEFAULT, WINIT_KAIMING = 0, 1
 
 
-class ConvUnit(ctypes.Structure):
-    """lrs_conv_unit: [upsample x2] -> pad -> conv(k, stride) -> [BN_lip] -> act."""
+class DipNode(ctypes.Structure):
+    """lrs_dip_node: one node of the network DAG (include/lrspnp.h).  Tensor 0 is the input and
+    node i produces tensor i + 1."""
     _fields_ = [(n, ctypes.c_int32) for n in
-                ("cin", "cout", "k", "stride", "pad", "pad_mode", "upsample", "bn", "act")]
+                ("kind", "in0", "in1", "cout", "k", "stride", "pad", "pad_mode", "upsample", "bn", "act", "sn",
+                 "winit")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+def conv_node(src, cin_unused, cout, k, stride=1, up=0, bn=BN_LIP, act=ACT_LRELU, pad_mode=PAD_REFLECT, sn=1,
+              winit=WINIT_KAIMING):
+    return DipNode(NODE_CONV, src, 0, cout, k, stride, (k - 1) // 2, pad_mode, up, bn, act, sn, winit)
 
 
 class EsState(ctypes.Structure):
@@ -44,28 +54,73 @@ class EsState(ctypes.Structure):
                 ("var_acc", ctypes.c_double), ("last_var", ctypes.c_double)]
 
 
-def lipschitz_unet_units(c_in: int = 128, c_out: int = 128, hidden: int = 128,
-                         pad: str = "reflection") -> list[ConvUnit]:
-    """The 14 conv units of my_Lipschitz_Unet (my_Lipschitz_Unet.py:31-103).
+def lipschitz_unet_nodes(c_in: int = 128, c_out: int = 128, hidden: int = 128,
+                         pad: str = "reflection") -> list[DipNode]:
+    """The 14 conv units of my_Lipschitz_Unet (my_Lipschitz_Unet.py:31-103) as a chain.
 
     The reference hard-codes 128 everywhere; c_in / c_out generalise the first / last conv to
     other band counts (hidden stays 128), as SURVEY.md §8 a8 sizes the 196x196x198 config."""
     pm = PAD_REFLECT if pad == "reflection" else PAD_ZERO
+    nodes = []
 
-    def u(cin, cout, k, stride=1, up=0, bn=1, act=ACT_LRELU):
-        return ConvUnit(cin, cout, k, stride, (k - 1) // 2, pm, up, bn, act)
+    def u(cout, k, stride=1, up=0, bn=BN_LIP):
+        nodes.append(conv_node(len(nodes), 0, cout, k, stride, up, bn, ACT_LRELU, pm))
 
     h = hidden
-    units = [u(c_in, h, 3, 2), u(h, h, 3)]                      # d_1  (:31-39)
+    u(h, 3, 2); u(h, 3)                                          # d_1  (:31-39)
     for _ in range(3):                                          # d_2..d_4 (:40-66)
-        units += [u(h, h, 3, 2), u(h, h, 3)]
-    units += [u(h, h, 2, up=1), u(h, h, 2, up=1)]               # up_1, up_2 (:71-82)
-    units += [u(h, h, 3, up=1), u(h, h, 3, up=1)]               # up_3, up_4 (:83-94)
-    units += [u(h, h, 1), u(h, c_out, 1, bn=0)]                 # last (:96-103)
-    return units
+        u(h, 3, 2); u(h, 3)
+    u(h, 2, up=1); u(h, 2, up=1)                                # up_1, up_2 (:71-82)
+    u(h, 3, up=1); u(h, 3, up=1)                                # up_3, up_4 (:83-94)
+    u(h, 1); u(c_out, 1, bn=BN_NONE)                            # last (:96-103)
+    return nodes
 
 
-# reference state_dict prefixes of each unit's conv / bn (named_parameters of my_Lipschitz_Unet)
+# backwards-compatible name
+lipschitz_unet_units = lipschitz_unet_nodes
+
+
+def skip_nodes(c_in: int = 128, c_out: int = 128, down=(128,) * 5, up=(128,) * 5, skip=(128,) * 5,
+               filter_down: int = 3, filter_up: int = 3, filter_skip: int = 1, pad: str = "reflection",
+               need_sigmoid: bool = True, need1x1_up: bool = True) -> list[DipNode]:
+    """models/skip.py:5-99 (the DIP net of main_LRS_PnP_DIP_pro.py:215-221) as a DAG.
+
+    Per scale i with input x:  out_i = act(BN(conv1x1(act(BN(conv3x3(BN(cat(skip_i(x),
+    up2(deeper_i(x)))))))))) where skip_i = act(BN(conv1x1 x)), deeper_i = act(BN(conv3x3(
+    act(BN(conv3x3 stride 2 (x)))))) followed by scale i+1 (not at the deepest); the final 1x1
+    conv + Sigmoid.  Plain BatchNorm2d, nn.Conv2d default init, no spectral norm."""
+    pm = PAD_REFLECT if pad == "reflection" else PAD_ZERO
+    nodes: list[DipNode] = []
+
+    def add(nd):
+        nodes.append(nd)
+        return len(nodes)          # tensor id of its output
+
+    def conv(src, cout, k, stride=1, bn=BN_PLAIN, act=ACT_LRELU):
+        return add(DipNode(NODE_CONV, src, 0, cout, k, stride, (k - 1) // 2, pm, 0, bn, act, 0, WINIT_DEFAULT))
+
+    def level(i, x):
+        s = conv(x, skip[i], filter_skip) if skip[i] else None                  # skip.py:57-60
+        d = conv(x, down[i], filter_down, 2)                                   # :63-65
+        d = conv(d, down[i], filter_down)                                      # :67-69
+        if i < len(down) - 1:
+            d = level(i + 1, d)                                                # deeper_main (:71-78)
+        if s is not None:
+            c = add(DipNode(NODE_CONCAT, s, d, 0, 0, 0, 0, 0, 1, 0, ACT_NONE, 0, 0))   # Concat + Upsample
+        else:
+            raise NotImplementedError("num_channels_skip = 0 (no Concat) is not used by the reference")
+        c = add(DipNode(NODE_BN, c, 0, 0, 0, 0, 0, 0, 0, BN_PLAIN, ACT_NONE, 0, 0))      # bn(skip + k) (:55)
+        c = conv(c, up[i], filter_up)                                           # :82-84
+        if need1x1_up:
+            c = conv(c, up[i], 1)                                               # :87-90
+        return c
+
+    top = level(0, 0)
+    conv(top, c_out, 1, bn=BN_NONE, act=ACT_SIGMOID if need_sigmoid else ACT_NONE)   # :95-97
+    return nodes
+
+
+# reference state_dict prefixes of each conv node of my_Lipschitz_Unet (named_parameters)
 UNET_REF_NAMES = (
     [("d_%d.0.1.module" % i, "d_%d.1" % i) if j == 0 else ("d_%d.3.1.module" % i, "d_%d.4" % i)
      for i in range(1, 5) for j in range(2)]
@@ -86,14 +141,14 @@ def _check(rc, what):
 class DipNet:
     """A sequential conv net on the HIP engine (lrs_dipnet_*), with flat parameter buffers."""
 
-    def __init__(self, units: list[ConvUnit], H: int, W: int, device="cuda"):
+    def __init__(self, nodes: list[DipNode], C: int, H: int, W: int, device="cuda"):
         import torch
 
         self.L = _lib.device_lib()
-        self.units = list(units)
-        arr = (ConvUnit * len(units))(*units)
+        self.units = self.nodes = list(nodes)
+        arr = (DipNode * len(nodes))(*nodes)
         h = ctypes.c_void_p()
-        _check(self.L.lrs_dipnet_create(arr, len(units), H, W, ctypes.byref(h)), "lrs_dipnet_create")
+        _check(self.L.lrs_dipnet_create(arr, len(nodes), C, H, W, ctypes.byref(h)), "lrs_dipnet_create")
         self.h = h
         self.H, self.W = H, W
         self.n_params = int(self.L.lrs_dipnet_num_params(h))
@@ -112,9 +167,14 @@ class DipNet:
         c, ho, wo = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         self.L.lrs_dipnet_out_shape(h, ctypes.byref(c), ctypes.byref(ho), ctypes.byref(wo))
         self.out_shape = (c.value, ho.value, wo.value)
-        self.in_shape = (units[0].cin, H, W)
+        self.in_shape = (C, H, W)
+        self.shapes = []
+        for i in range(len(nodes)):
+            cc, hh, ww = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            self.L.lrs_dipnet_node_shape(h, i, ctypes.byref(cc), ctypes.byref(hh), ctypes.byref(ww))
+            self.shapes.append((cc.value, hh.value, ww.value))
         self.offsets = []
-        for i in range(len(units)):
+        for i in range(len(nodes)):
             o = [ctypes.c_int64() for _ in range(4)]
             self.L.lrs_dipnet_param_offsets(h, i, *[ctypes.byref(x) for x in o])
             self.offsets.append(tuple(x.value for x in o))
@@ -136,13 +196,17 @@ class DipNet:
                                              ctypes.c_void_p(self.stream.cuda_stream)), "init_params")
 
     def param_views(self, i: int, flat=None):
-        """(weight [cout,cin,k,k], bias, gamma|None, beta|None) views into `flat` (default params)."""
+        """(weight [cout,cin,k,k] | None, bias | None, gamma | None, beta | None) of node i, as views
+        into `flat` (default: the parameters)."""
         flat = self.params if flat is None else flat
-        u = self.units[i]
+        nd = self.nodes[i]
         w, b, g, be = self.offsets[i]
-        kk = u.cin * u.k * u.k
-        out = [flat[w:w + u.cout * kk].view(u.cout, u.cin, u.k, u.k), flat[b:b + u.cout]]
-        out += [flat[g:g + u.cout] if g >= 0 else None, flat[be:be + u.cout] if be >= 0 else None]
+        C = self.shapes[i][0]
+        out = [None, None]
+        if nd.kind == NODE_CONV:
+            cin = self.in_shape[0] if nd.in0 == 0 else self.shapes[nd.in0 - 1][0]
+            out = [flat[w:w + C * cin * nd.k * nd.k].view(C, cin, nd.k, nd.k), flat[b:b + C]]
+        out += [flat[g:g + C] if g >= 0 else None, flat[be:be + C] if be >= 0 else None]
         return tuple(out)
 
     def load_reference_state_dict(self, sd, names=UNET_REF_NAMES):
@@ -248,19 +312,23 @@ class DipConfig:
     use_graph: bool = False       # replay one captured hipGraph per step (measured slower than
                                   # direct launches on ROCm 7.2 for this ~110-kernel step)
     hidden: int = 128
+    net: str = "unet1lip"         # 'unet1lip' (…1-LiP.py:214) or 'skip' (…pro.py:215-221)
     early_stop: bool = True       # False: exactly num_iter steps (the timed-benchmark mode, §8d)
 
 
-class LipschitzDip:
-    """get_DIP_out on the HIP engine; one network object reused across outer iterations
-    (re-initialised each call, as the reference builds a fresh net per call)."""
+class DipProx:
+    """get_DIP_out on the HIP engine (…1-LiP.py:208-264 with my_Lipschitz_Unet, …pro.py:211-272
+    with skip()); one network object reused across outer iterations (re-initialised each call,
+    as the reference builds a fresh net per call)."""
 
     def __init__(self, bands: int, H: int, W: int, cfg: DipConfig | None = None, device="cuda"):
         self.cfg = cfg or DipConfig()
-        self.net = DipNet(lipschitz_unet_units(bands, bands, self.cfg.hidden), H, W, device=device)
+        nodes = (skip_nodes(bands, bands) if self.cfg.net == "skip"
+                 else lipschitz_unet_nodes(bands, bands, self.cfg.hidden))
+        self.net = DipNet(nodes, bands, H, W, device=device)
         if self.net.out_shape != (bands, H, W):
-            raise ValueError(f"my_Lipschitz_Unet maps {H}x{W} to {self.net.out_shape[1:]}; the reference "
-                             "architecture needs sizes it reproduces (e.g. 36, 196)")
+            raise ValueError(f"the DIP net maps {H}x{W} to {self.net.out_shape[1:]}; the reference "
+                             "architecture needs sizes it reproduces (e.g. 36, 196 for the U-Net)")
         self.es = EarlyStopper(bands * H * W, self.cfg.es_size, self.cfg.patience, device=device)
         self.calls = 0
         self.last_steps = 0
@@ -306,6 +374,9 @@ class LipschitzDip:
         return self.es.slot_of(st.count - 1).view(net.out_shape)
 
 
+LipschitzDip = DipProx   # the 1-Lip name used by the first callers
+
+
 def dip_input_from_unfolded(Z, H: int, W: int):
     """(P, B) unfolded matrix (p = i + H j) -> (B, H, W) image (…1-LiP.py:404)."""
     B = Z.shape[1]
@@ -347,10 +418,11 @@ def out_size(H, W, k, stride, pad, up):
 def unet_size_ok(H: int, W: int) -> bool:
     """True when my_Lipschitz_Unet maps H x W back to H x W."""
     h, w = H, W
-    for u in lipschitz_unet_units(1, 1, 1):
+    for u in lipschitz_unet_nodes(1, 1, 1):
         h, w = out_size(h, w, u.k, u.stride, u.pad, u.upsample)
     return (h, w) == (H, W)
 
 
-__all__ = ["ConvUnit", "DipNet", "EarlyStopper", "DipConfig", "LipschitzDip", "lipschitz_unet_units",
+__all__ = ["DipNode", "DipNet", "EarlyStopper", "DipConfig", "DipProx", "LipschitzDip", "lipschitz_unet_nodes",
+           "lipschitz_unet_units", "skip_nodes",
            "UNET_REF_NAMES", "dip_input_from_unfolded", "unfolded_from_image", "sigma_max", "unet_size_ok"]

@@ -45,6 +45,19 @@ class LrsPnPConfig:
         base.update(kw)
         return LrsPnPConfig(**base)
 
+    @staticmethod
+    def dip_pro(**kw) -> "LrsPnPConfig":
+        """main_LRS_PnP_DIP_pro.py:324-353: as dip_1lip, with the skip() network (5 scales of 128
+        channels, 128-channel skips, plain BatchNorm, Sigmoid) as the DIP prox (:215-221)."""
+        from .dip import DipConfig
+        dip = kw.pop("dip", None) or DipConfig(net="skip")
+        if dip.net != "skip":
+            raise LrsError("dip_pro uses the skip network")
+        base = dict(gamma=0.5, mu1=0.1, mu2=0.1, lambda_ista=0.1, Nit=100, bb=36, sliding=36, variant="fro4",
+                    lowrank="dip", dip=dip)
+        base.update(kw)
+        return LrsPnPConfig(**base)
+
 
 _ALPHA = {"spec2": ops.ALPHA_SPEC2, "fro4": ops.ALPHA_FRO4, "soft": ops.ALPHA_SOFT}
 

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(HERE, "golden"))
 
 import dip_ref  # noqa: E402
 from gen_dip_golden import flat_params, problem  # noqa: E402
-from lrspnp.dip import ConvUnit, lipschitz_unet_units, unet_size_ok  # noqa: E402
+from lrspnp.dip import DipNode, lipschitz_unet_units, skip_nodes, unet_size_ok  # noqa: E402
 
 
 def rel(a, b):
@@ -33,7 +33,7 @@ def test_restatement_matches_reference_unet(gold):
     flat = torch.from_numpy(flat_params(units, int(gold["seed"])))
     x, target, mask = (torch.from_numpy(a) for a in problem(int(gold["seed"])))
     # sigma_max of every conv (SpectralNorm._update_u_v)
-    offs, _ = dip_ref.param_offsets(units)
+    offs, _ = dip_ref.param_offsets(units, 128)
     sig = [float(dip_ref.sigma_scale(dip_ref.views(flat, units, i, offs)[0])[0]) for i in range(len(units))]
     np.testing.assert_allclose(sig, gold["sigma"], rtol=2e-6)
     tr = dip_ref.RefTrainer(units, flat, lr=0.1)
@@ -60,15 +60,43 @@ def test_restatement_matches_reference_unet(gold):
             np.testing.assert_allclose(gn[big], ref[big], rtol=1e-4)
 
 
+def test_restatement_matches_reference_skip(golden):
+    gold = golden("skip_golden.npz")
+    torch.manual_seed(0)
+    nodes = skip_nodes(128, 128)
+    flat = torch.from_numpy(flat_params(nodes, int(gold["seed"])))
+    x, target, mask = (torch.from_numpy(a) for a in problem(int(gold["seed"])))
+    tr = dip_ref.RefTrainer(nodes, flat, lr=0.1)
+    sub = int(gold["sub"])
+    out, loss, g = tr.step(x, target, mask)
+    assert abs(loss - gold["loss"][0]) <= 1e-6 * gold["loss"][0], (loss, gold["loss"][0])
+    assert rel(out.numpy().reshape(-1)[::sub], gold["out_sub"][0]) < 1e-5
+    # gradient norms per reference parameter, in parameters() order = the flat layout
+    offs, _ = dip_ref.param_offsets(nodes, 128)
+    gn = []
+    for i in range(len(nodes)):
+        for v in dip_ref.views(g, nodes, i, offs):
+            if v is not None:
+                gn.append(float(v.norm()))
+    gn, ref = np.array(gn), gold["grad_norms"]
+    assert gn.shape == ref.shape
+    big = ref > 1e-4 * ref.max()
+    np.testing.assert_allclose(gn[big], ref[big], rtol=1e-4)
+
+
 def test_engine_layout_matches_restatement():
     from lrspnp import _lib
     L = _lib.lib()
-    units = lipschitz_unet_units(128, 198, 128)
-    arr = (ConvUnit * len(units))(*units)
+    for units, c0, H in ((lipschitz_unet_units(198, 198, 128), 198, 196), (skip_nodes(128, 128), 128, 36)):
+        _check_layout(L, units, c0, H)
+
+
+def _check_layout(L, units, c0, H):
+    arr = (DipNode * len(units))(*units)
     h = ctypes.c_void_p()
-    assert L.lrs_dipnet_create(arr, len(units), 196, 196, ctypes.byref(h)) == 0
+    assert L.lrs_dipnet_create(arr, len(units), c0, H, H, ctypes.byref(h)) == 0
     try:
-        offs, n = dip_ref.param_offsets(units)
+        offs, n = dip_ref.param_offsets(units, c0, H, H)
         assert L.lrs_dipnet_num_params(h) == n
         for i, o in enumerate(offs):
             got = [ctypes.c_int64() for _ in range(4)]
@@ -76,7 +104,11 @@ def test_engine_layout_matches_restatement():
             assert tuple(x.value for x in got) == o
         c, ho, wo = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         L.lrs_dipnet_out_shape(h, ctypes.byref(c), ctypes.byref(ho), ctypes.byref(wo))
-        assert (c.value, ho.value, wo.value) == (198, 196, 196)
+        assert (c.value, ho.value, wo.value) == (c0, H, H)
+        sh = dip_ref.shapes(units, c0, H, H)
+        for i in range(len(units)):
+            L.lrs_dipnet_node_shape(h, i, ctypes.byref(c), ctypes.byref(ho), ctypes.byref(wo))
+            assert (c.value, ho.value, wo.value) == sh[i + 1]
         assert L.lrs_dipnet_workspace(h) > 0
     finally:
         L.lrs_dipnet_destroy(h)
