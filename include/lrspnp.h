@@ -92,6 +92,14 @@ int lrs_ista_alpha_f32(const float *D, int64_t n, int64_t K, const uint8_t *obs_
 int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,
                  int64_t K, int64_t nb, const float *alpha, const double *thr, int Nit, int prox,
                  float *coefs, float *phi, void *stream);
+/* Arithmetic of the two products of the resident (n_pad <= 64) kernel, process-wide:
+ * LRS_ISTA_SPLIT_BF16 (default): bf16 matrix cores on operands split exactly into three bf16
+ * terms (six partial products, fp32 accumulation: fp32-GEMM accuracy, not bitwise the f32 MFMA);
+ * LRS_ISTA_F32: v_mfma_f32_16x16x4_f32 (exact f32 products).  The NLM prox is identical. */
+#define LRS_ISTA_F32 0
+#define LRS_ISTA_SPLIT_BF16 1
+int lrs_ista_set_precision(int precision);
+int lrs_ista_get_precision(void);
 
 /* ---- SVT low-rank prox ---------------------------------------------------------------------
  * U = SVT(Z, tau) with Z = X + c2 * L2 (c2 = float(1/mu_2); L2 may be NULL), via an fp64 Gram

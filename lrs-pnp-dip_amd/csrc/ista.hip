@@ -382,6 +382,274 @@ __global__ __launch_bounds__(kIstaThreads, 2) void k_ista_res(IstaParams p) {
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Split-bf16 resident kernel (n_pad <= 64, K = 256).  The two products per inner iteration run on
+// the bf16 matrix cores (v_mfma_f32_16x16x32_bf16, 16x the f32 MFMA rate, and unlike the f32
+// MFMA not on the VALU's FMA datapath) with every fp32 operand split exactly into three bf16
+// terms, v = v1 + v2 + v3 (8 significand bits each: 24 = fp32); the six products with
+// i + j <= 4 are kept (the dropped ones are <= 2^-24 relative), accumulated in fp32, so each
+// product has fp32-GEMM accuracy (not the bitwise f32 MFMA result; parity is held to the same
+// 1e-5 relative L2 as the rest of the pipeline).
+//   * D lives in LDS once, as three bf16 images [row][atom] with 8-byte chunks XOR-swizzled per
+//     row; the first product reads its A fragments by rows (ds_read_b64), the second reads the
+//     same images transposed (ds_read_b64_tr_b16): 96 KB instead of the f32 kernel's 136 KB;
+//   * accumulators feed the next product's B operand directly (C rows 4g..4g+3 of two 16-tiles
+//     = the 8 k-values of lane group g), as in the f32 kernel.
+// ------------------------------------------------------------------------------------------------
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+
+template <int K>
+struct alignas(16) IstaSmemB3 {
+    __bf16 D[3][kStageRows][K];   // split s of D, [row][atom], chunk-swizzled
+};
+
+// XOR swizzle of the 8-byte chunk index by row (linear over GF(2) in row & 15): conflict-free for
+// the 32-lane halves of both the row reads and the transposed reads (searched exhaustively)
+__device__ __forceinline__ int b3_swz(int row) {
+    return ((row & 1) ? 26 : 0) ^ ((row & 2) ? 12 : 0) ^ ((row & 4) ? 62 : 0) ^ ((row & 8) ? 3 : 0);
+}
+
+template <int K>
+__device__ __forceinline__ int b3_off(int row, int chunk) {   // element offset within one image
+    return row * K + 4 * (chunk ^ b3_swz(row));
+}
+
+__device__ __forceinline__ void split3(float v, __bf16 &a, __bf16 &b, __bf16 &c) {
+    a = (__bf16)v;
+    const float r1 = v - (float)a;
+    b = (__bf16)r1;
+    const float r2 = r1 - (float)b;
+    c = (__bf16)r2;
+}
+
+constexpr int kB3Waves = 4;                       // one wave per SIMD: the whole 512-entry register file
+constexpr int kB3Threads = kB3Waves * kWave;
+
+template <int K>
+__device__ __forceinline__ void stage_dictionary_b3(IstaSmemB3<K> &S, const float *__restrict__ D, int n) {
+    for (int idx = threadIdx.x; idx < kStageRows * K; idx += kB3Threads) {
+        const int r = idx / K, a = idx % K;
+        const float v = r < n ? D[(int64_t)r * K + a] : 0.0f;
+        __bf16 h, m, l;
+        split3(v, h, m, l);
+        const int o = b3_off<K>(r, a >> 2) + (a & 3);
+        S.D[0][0][o] = h;
+        S.D[1][0][o] = m;
+        S.D[2][0][o] = l;
+    }
+}
+
+// 8 bf16 per split from 2 x 4 fp32 (elements 0..3 = u, 4..7 = w)
+__device__ __forceinline__ void split_frag(const float (&u)[4], const float (&w)[4], bf16x8 (&f)[3]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        __bf16 a, b, c;
+        split3(u[e], a, b, c);
+        f[0][e] = a; f[1][e] = b; f[2][e] = c;
+        split3(w[e], a, b, c);
+        f[0][e + 4] = a; f[1][e + 4] = b; f[2][e + 4] = c;
+    }
+}
+
+__device__ __forceinline__ floatx4 mfma_bf(const bf16x8 &a, const bf16x8 &b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// acc += A B with both split three ways, small terms first
+__device__ __forceinline__ floatx4 mfma_split6(const bf16x8 (&A)[3], const bf16x8 (&B)[3], floatx4 acc) {
+    acc = mfma_bf(A[2], B[0], acc);
+    acc = mfma_bf(A[1], B[1], acc);
+    acc = mfma_bf(A[0], B[2], acc);
+    acc = mfma_bf(A[1], B[0], acc);
+    acc = mfma_bf(A[0], B[1], acc);
+    acc = mfma_bf(A[0], B[0], acc);
+    return acc;
+}
+
+__device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+// G tile q = D^T r: A = D^T rows (atoms 16q..16q+15) by transposed reads, B = r split, per row pair
+template <int K>
+__device__ __forceinline__ floatx4 b3_gemm2(const IstaSmemB3<K> &S, int q, const bf16x8 (&rf)[2][3], int lane) {
+    const int g = lane >> 4, ll = lane & 15, qq = ll >> 2, pp = ll & 3;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+        const int r0 = 32 * pr + 4 * g + qq, r1 = r0 + 16;
+        bf16x8 A[3];
+#pragma unroll
+        for (int sp = 0; sp < 3; ++sp) {
+            typedef __attribute__((address_space(3))) short4v lds_s4;
+            const short4v a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s4 *)(&S.D[sp][0][b3_off<K>(r0, 4 * q + pp)]));
+            const short4v a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s4 *)(&S.D[sp][0][b3_off<K>(r1, 4 * q + pp)]));
+            A[sp] = cat4(__builtin_bit_cast(bf16x4, a0), __builtin_bit_cast(bf16x4, a1));
+        }
+        acc = mfma_split6(A, rf[pr], acc);
+    }
+    return acc;
+}
+
+// R[t] += D rows (16t..) x (atom tiles 2p, 2p+1): A = D rows by row reads, B = x split
+template <int K>
+__device__ __forceinline__ void b3_gemm1(const IstaSmemB3<K> &S, int p, const bf16x8 (&xf)[3], floatx4 (&R)[4],
+                                         int lane) {
+    const int g = lane >> 4, ll = lane & 15;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int row = 16 * t + ll;
+        bf16x8 A[3];
+#pragma unroll
+        for (int sp = 0; sp < 3; ++sp) {
+            const bf16x4 a0 = *reinterpret_cast<const bf16x4 *>(&S.D[sp][0][b3_off<K>(row, 8 * p + g)]);
+            const bf16x4 a1 = *reinterpret_cast<const bf16x4 *>(&S.D[sp][0][b3_off<K>(row, 8 * p + 4 + g)]);
+            A[sp] = cat4(a0, a1);
+        }
+        R[t] = mfma_split6(A, xf, R[t]);
+    }
+}
+
+template <int K, bool SOFT>
+__global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
+    static_assert(K == 256, "the chunk swizzle assumes 64 chunks per row");
+    constexpr int NQ = K / 16;
+    __shared__ __attribute__((aligned(16))) IstaSmemB3<K> S;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int jl = lane & 15, g = lane >> 4;
+    const int64_t j = ((int64_t)blockIdx.x * kB3Waves + wave) * 16 + jl;
+    const bool valid = j < p.nb;
+    const int NT = p.n_pad / 16;
+    const NlmLanes L(lane);
+
+    const float alpha = valid ? p.alpha[j] : 1.0f;
+    const double thr = valid ? p.thr[j] : 1.0;
+    const double kneg = nlm_kneg(thr);
+    const double c0 = nlm_c0();
+    const float Tsoft = (float)thr;
+
+    float y[4][4];
+    uint32_t mres = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        float4 yv = {0.f, 0.f, 0.f, 0.f};
+        uint32_t mv = 0;
+        if (valid && t < NT) {
+            yv = *reinterpret_cast<const float4 *>(&p.Yb[j * p.n_pad + 16 * t + 4 * g]);
+            mv = *reinterpret_cast<const uint32_t *>(&p.obs[j * p.n_pad + 16 * t + 4 * g]);
+        }
+        y[t][0] = yv.x; y[t][1] = yv.y; y[t][2] = yv.z; y[t][3] = yv.w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mres |= (((mv >> (8 * i)) & 0xffu) ? 1u : 0u) << (4 * t + i);
+    }
+    stage_dictionary_b3<K>(S, p.D, p.n);
+    __syncthreads();
+
+    float X[NQ][4];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) X[q][0] = X[q][1] = X[q][2] = X[q][3] = 0.f;
+    floatx4 R[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const float ainv = 1.0f / alpha;
+    auto gradient = [&](floatx4 &Gq, const float (&xq)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Gq[i] = xq[i] + div_by(Gq[i], alpha, ainv);
+    };
+
+    for (int it = 0; it < p.Nit; ++it) {
+        float r[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[t][i] = ((mres >> (4 * t + i)) & 1u) ? (y[t][i] - R[t][i]) : 0.0f;
+            R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        bf16x8 rf[2][3];
+        split_frag(r[0], r[1], rf[0]);
+        split_frag(r[2], r[3], rf[1]);
+        // pipeline over tile pairs: step p runs the products of tiles 2p+4, 2p+5 and the
+        // (independent, so interleavable) NLM of tiles 2p and 2p+1 on one wave's instruction stream
+        floatx4 G[NQ];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) G[q] = b3_gemm2<K>(S, q, rf, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gradient(G[q], X[q]);
+        float Pprev[3] = {0.f, 0.f, 0.f}, Ncur[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Ncur[e] = __shfl(G[0][e], L.src_next, 64);
+#pragma unroll
+        for (int pp = 0; pp < NQ / 2; ++pp) {
+            const int qa = 2 * pp, qb = qa + 1;
+            if (qa + 4 < NQ) G[qa + 4] = b3_gemm2<K>(S, qa + 4, rf, lane);
+            if (qb + 4 < NQ) G[qb + 4] = b3_gemm2<K>(S, qb + 4, rf, lane);
+            float oa[4], ob[4];
+            if (SOFT) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float t = fabsf(G[qa][i]) - Tsoft;
+                    t = t > 0.f ? t : 0.f;
+                    oa[i] = G[qa][i] > 0.f ? t : (G[qa][i] < 0.f ? -t : 0.f);
+                    float u = fabsf(G[qb][i]) - Tsoft;
+                    u = u > 0.f ? u : 0.f;
+                    ob[i] = G[qb][i] > 0.f ? u : (G[qb][i] < 0.f ? -u : 0.f);
+                }
+            } else {
+                const float owna[4] = {G[qa][0], G[qa][1], G[qa][2], G[qa][3]};
+                const float ownb[4] = {G[qb][0], G[qb][1], G[qb][2], G[qb][3]};
+                float Pa[3], Pb[3], Nb[4], Nn[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int e = 0; e < 3; ++e) {
+                    Pa[e] = __shfl(G[qa][e + 1], L.src_prev, 64);
+                    Pb[e] = __shfl(G[qb][e + 1], L.src_prev, 64);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Nb[e] = __shfl(G[qb][e], L.src_next, 64);
+                if (qb + 1 < NQ) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) Nn[e] = __shfl(G[qb + 1][e], L.src_next, 64);
+                }
+                nlm_tile<NQ>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, oa);
+                nlm_tile<NQ>(qb, L, ownb, Pa, Pb, Nb, Nn, kneg, c0, ob);
+#pragma unroll
+                for (int e = 0; e < 3; ++e) Pprev[e] = Pb[e];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Ncur[e] = Nn[e];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { X[qa][i] = oa[i]; X[qb][i] = ob[i]; }
+            {
+                bf16x8 xf[3];
+                split_frag(X[qa], X[qb], xf);
+                b3_gemm1<K>(S, pp, xf, R, lane);
+            }
+            if (qa + 4 < NQ) gradient(G[qa + 4], X[qa + 4]);
+            if (qb + 4 < NQ) gradient(G[qb + 4], X[qb + 4]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    if (valid) {
+        if (p.coefs) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                *reinterpret_cast<float4 *>(&p.coefs[j * K + 16 * q + 4 * g]) =
+                    make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t < NT)
+                *reinterpret_cast<float4 *>(&p.phi[j * p.n_pad + 16 * t + 4 * g]) =
+                    make_float4(R[t][0], R[t][1], R[t][2], R[t][3]);
+    }
+}
+
 template <int K, bool RESIDENT>
 __global__ __launch_bounds__(kIstaThreads, 2) void k_ista(IstaParams p) {
     constexpr int NQ = K / 16;
@@ -545,6 +813,17 @@ __global__ __launch_bounds__(256) void k_nlm_col(const float *__restrict__ g, in
 
 using namespace lrs;
 
+// precision of the resident kernel's two products: LRS_ISTA_SPLIT_BF16 (default) or LRS_ISTA_F32
+static int g_ista_precision = LRS_ISTA_SPLIT_BF16;
+
+extern "C" int lrs_ista_set_precision(int precision) {
+    if (precision != LRS_ISTA_F32 && precision != LRS_ISTA_SPLIT_BF16) return LRS_E_INVALID;
+    g_ista_precision = precision;
+    return LRS_OK;
+}
+
+extern "C" int lrs_ista_get_precision(void) { return g_ista_precision; }
+
 extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n,
                             int64_t n_pad, int64_t K, int64_t nb, const float *alpha, const double *thr,
                             int Nit, int prox, float *coefs, float *phi, void *stream) {
@@ -558,7 +837,13 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
     dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));
     hipStream_t st = (hipStream_t)stream;
-    if (n_pad <= kStageRows && prox == LRS_PROX_SOFT)
+    const bool split = g_ista_precision == LRS_ISTA_SPLIT_BF16;
+    const dim3 grid_b3((unsigned)((nb + kB3Waves * 16 - 1) / (kB3Waves * 16)));
+    if (n_pad <= kStageRows && split && prox == LRS_PROX_SOFT)
+        hipLaunchKernelGGL((k_ista_b3<256, true>), grid_b3, dim3(kB3Threads), 0, st, p);
+    else if (n_pad <= kStageRows && split)
+        hipLaunchKernelGGL((k_ista_b3<256, false>), grid_b3, dim3(kB3Threads), 0, st, p);
+    else if (n_pad <= kStageRows && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_res<256, true>), grid, dim3(kIstaThreads), 0, st, p);
     else if (n_pad <= kStageRows)
         hipLaunchKernelGGL((k_ista_res<256, false>), grid, dim3(kIstaThreads), 0, st, p);

@@ -221,3 +221,34 @@ def test_admm_update_bitexact_vs_oracle(ops):
         nref = [np.sum((Xo.astype(np.float64) - X) ** 2), np.sum((L1o.astype(np.float64) - L1) ** 2),
                 np.sum((L2o.astype(np.float64) - L2) ** 2)]
         assert np.allclose(norms.cpu().numpy(), nref, rtol=1e-10)
+
+
+def test_ista_both_product_precisions_match_oracle():
+    """The resident kernel's products in exact f32 MFMA and in split-bf16 MFMA (the default):
+    both within 1e-5 of the oracle, and within 1e-6 of each other."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lrspnp import _lib, ops
+    from lrspnp.data import synthetic_dictionary
+    L = _lib.device_lib()
+    rng = np.random.default_rng(11)
+    nb, n = 300, 64
+    D = synthetic_dictionary(n, 256, 0)
+    Yb = (rng.standard_normal((nb, n)) * 0.3).astype(np.float32)
+    obs = (rng.random((nb, n)) > 0.1).astype(np.uint8)
+    Yb[obs == 0] = 0
+    Dd, Yd, od = (torch.from_numpy(a).cuda() for a in (D, Yb, obs))
+    alpha, thr = ops.ista_alpha(Dd, od, n, ops.ALPHA_SPEC2, 0.1)
+    al, th = alpha.cpu().numpy(), thr.cpu().numpy()
+    coefs_o, phi_o = O.ista_batch(Yb, obs, D, al, th, 30)
+    out = {}
+    try:
+        for prec in (0, 1):
+            assert L.lrs_ista_set_precision(prec) == 0
+            phi, coefs = ops.ista(Yd, od, Dd, n, alpha, thr, 30, ops.PROX_NLM, want_coefs=True)
+            torch.cuda.synchronize()
+            out[prec] = (phi.cpu().numpy()[:, :n], coefs.cpu().numpy())
+            assert rel(out[prec][0], phi_o) < 1e-5 and rel(out[prec][1], coefs_o) < 1e-5
+    finally:
+        L.lrs_ista_set_precision(1)
+    assert rel(out[1][0], out[0][0]) < 1e-6

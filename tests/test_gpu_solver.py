@@ -65,7 +65,7 @@ def test_dip_variant_sparse_coding_matches_oracle(gpu, golden):
     Y = unfold(d["noisy"][0])
     M = mask_matrix(d["lrs_mask"], 128)
     D = synthetic_dictionary(1296, 256, 0)
-    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_1lip())
+    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_1lip(lowrank="svt"))   # the sparse-coding half only
     phi = s.sparse_coding().cpu().numpy()[:, :1296]
     o = O.LrsPnpOracle(Y, M, D, bb=36, sliding=36, gamma=0.5, mu1=0.1, mu2=0.1, Nit=100, variant="fro4")
     blocks = O.im2col(o.X + o.L1 / np.float32(0.1), 36, o.rows, o.cols)
