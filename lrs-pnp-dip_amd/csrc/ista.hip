@@ -513,6 +513,122 @@ __device__ __forceinline__ void b3_gemm1(const IstaSmemB3<K> &S, int p, const bf
     }
 }
 
+
+// ---- NLM chunk with weight reuse (split-bf16 kernel) ---------------------------------------------
+// Chunk c's weights W1[2], W2[1..2], W3[0..2] (pairs starting left of the chunk) equal chunk c-1's
+// W1[6], W2[5..6], W3[4..6], so a lane computes 12 of the 18 weights and takes the other 6 (hi
+// words) from lane l-16 (chunk c-1).  Weights are bitwise the same as nlm_chunk's.  The weight sums
+// are exact in fp64 (<= 6 terms of 21 significant bits within 8 binades), so their order is free;
+// num/den uses one Newton step on v_rcp_f64 and a remainder correction (|error| < 1 ulp of fp64
+// before the final float rounding, instead of the IEEE division sequence).
+struct Reuse6 {
+    int v[6];   // W1[6], W2[5], W2[6], W3[4], W3[5], W3[6] of a chunk
+};
+
+__device__ __forceinline__ float nlm_div_fast(double num, double den) {
+    double r = __builtin_amdgcn_rcp(den);
+    const double e = __fma_rn(-den, r, 1.0);
+    r = __fma_rn(r, e, r);
+    const double q = num * r;
+    const double rem = __fma_rn(-den, q, num);
+    return (float)__fma_rn(rem, r, q);
+}
+
+// W_t[i] = weight(s_t(i) + s_t(i+1)), s_t(k) = (w[k] - w[k+t])^2, for i >= i0 (FULL: all 18)
+template <bool FULL>
+__device__ __forceinline__ void nlm_weights(const double (&w)[11], double kneg, int (&W1)[7], int (&W2)[7],
+                                            int (&W3)[7]) {
+    {
+        constexpr int i0 = FULL ? 2 : 3;
+        double sp = (w[i0] - w[i0 + 1]) * (w[i0] - w[i0 + 1]);
+#pragma unroll
+        for (int i = i0; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 2], sn = d * d;
+            W1[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
+    {
+        constexpr int i0 = FULL ? 1 : 3;
+        double sp = (w[i0] - w[i0 + 2]) * (w[i0] - w[i0 + 2]);
+#pragma unroll
+        for (int i = i0; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 3], sn = d * d;
+            W2[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
+    {
+        constexpr int i0 = FULL ? 0 : 3;
+        double sp = (w[i0] - w[i0 + 3]) * (w[i0] - w[i0 + 3]);
+#pragma unroll
+        for (int i = i0; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 4], sn = d * d;
+            W3[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
+}
+
+__device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W1)[7], const int (&W2)[7],
+                                            const int (&W3)[7], double c0, float (&out)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int C = 3 + e;
+        const double ws[6] = {hi_to_double(W3[C - 3]), hi_to_double(W2[C - 2]), hi_to_double(W1[C - 1]),
+                              hi_to_double(W1[C]), hi_to_double(W2[C]), hi_to_double(W3[C])};
+        const double vs[6] = {w[C - 3], w[C - 2], w[C - 1], w[C + 1], w[C + 2], w[C + 3]};
+        double swv = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) swv = __fma_rn(ws[k], vs[k], swv);   // canonical order
+        const double sw = ((ws[0] + ws[5]) + (ws[1] + ws[4])) + (ws[2] + ws[3]);   // exact
+        const double num = __fma_rn(7.0, swv, c0 * w[C]);
+        const double den = __fma_rn(7.0, sw, c0);
+        out[e] = nlm_div_fast(num, den);
+    }
+}
+
+// tile q of the NLM with weight reuse (FULL for the first tile, whose g == 0 chunk has a
+// reflected window).  `carry`: this lane's trailing weights of tile q-1 on entry, of tile q on
+// exit; only the g == 3 lanes' copy is read (by the g == 0 lanes of the next tile).
+template <int NQ, bool FULL>
+__device__ __forceinline__ void nlm_tile_reuse(int q, const NlmLanes &L, const float (&own)[4], const float (&Pprev)[3],
+                                               const float (&Pcur)[3], const float (&Ncur)[4], const float (&Nnext)[4],
+                                               double kneg, double c0, Reuse6 &carry, float (&out)[4]) {
+    float prv[3], nxt[4];
+    if (L.g == 0) {
+        if (q == 0) { prv[0] = own[3]; prv[1] = own[2]; prv[2] = own[1]; }
+        else { prv[0] = Pprev[0]; prv[1] = Pprev[1]; prv[2] = Pprev[2]; }
+    } else {
+        prv[0] = Pcur[0]; prv[1] = Pcur[1]; prv[2] = Pcur[2];
+    }
+    if (L.g == 3) {
+        if (q == NQ - 1) { nxt[0] = own[2]; nxt[1] = own[1]; nxt[2] = own[0]; nxt[3] = prv[2]; }
+        else { nxt[0] = Nnext[0]; nxt[1] = Nnext[1]; nxt[2] = Nnext[2]; nxt[3] = Nnext[3]; }
+    } else {
+        nxt[0] = Ncur[0]; nxt[1] = Ncur[1]; nxt[2] = Ncur[2]; nxt[3] = Ncur[3];
+    }
+    const double w[11] = {prv[0], prv[1], prv[2], own[0], own[1], own[2], own[3],
+                          nxt[0], nxt[1], nxt[2], nxt[3]};
+    int W1[7], W2[7], W3[7];
+    nlm_weights<FULL>(w, kneg, W1, W2, W3);
+    if (!FULL) {
+        // chunk c-1 is lane l-16's chunk of this tile (g >= 1) or lane l+48's chunk of tile q-1
+        // (g == 0): the g == 3 source serves its tile q-1 weights
+        const int mine[6] = {W1[6], W2[5], W2[6], W3[4], W3[5], W3[6]};
+        int prev[6];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) prev[e] = __shfl((L.g == 3) ? carry.v[e] : mine[e], L.src_prev, 64);
+        W1[2] = prev[0];
+        W2[1] = prev[1]; W2[2] = prev[2];
+        W3[0] = prev[3]; W3[1] = prev[4]; W3[2] = prev[5];
+    }
+    carry.v[0] = W1[6];
+    carry.v[1] = W2[5]; carry.v[2] = W2[6];
+    carry.v[3] = W3[4]; carry.v[4] = W3[5]; carry.v[5] = W3[6];
+    nlm_outputs(w, W1, W2, W3, c0, out);
+}
+
 template <int K, bool SOFT>
 __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
     static_assert(K == 256, "the chunk swizzle assumes 64 chunks per row");
@@ -582,6 +698,7 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) gradient(G[q], X[q]);
         float Pprev[3] = {0.f, 0.f, 0.f}, Ncur[4];
+        Reuse6 carry{};
 #pragma unroll
         for (int e = 0; e < 4; ++e) Ncur[e] = __shfl(G[0][e], L.src_next, 64);
 #pragma unroll
@@ -615,8 +732,9 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) Nn[e] = __shfl(G[qb + 1][e], L.src_next, 64);
                 }
-                nlm_tile<NQ>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, oa);
-                nlm_tile<NQ>(qb, L, ownb, Pa, Pb, Nb, Nn, kneg, c0, ob);
+                if (qa == 0) nlm_tile_reuse<NQ, true>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, carry, oa);
+                else nlm_tile_reuse<NQ, false>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, carry, oa);
+                nlm_tile_reuse<NQ, false>(qb, L, ownb, Pa, Pb, Nb, Nn, kneg, c0, carry, ob);
 #pragma unroll
                 for (int e = 0; e < 3; ++e) Pprev[e] = Pb[e];
 #pragma unroll
