@@ -259,6 +259,12 @@ int lrs_dipnet_train_steps(lrs_dipnet *net, const float *x, const float *target,
 /* loss of the last step (synchronises the stream; diagnostics only) */
 int lrs_dipnet_last_loss(lrs_dipnet *net, double *loss, void *stream);
 
+/* ---- Metrics (not timed) -------------------------------------------------------------------
+ * acc (device double) = sum of the SSIM map of pytorch_ssim.ssim(img1, img2) over C x H x W
+ * (pytorch_ssim/__init__.py:17-37; called at main_LRS_PnP_DIP_1-LiP.py:480-481); MSSIM =
+ * acc / (C*H*W).  Images are [C][H][W] float32. */
+int lrs_ssim_f32(const float *img1, const float *img2, int C, int H, int W, double *acc, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

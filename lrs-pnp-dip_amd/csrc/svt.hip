@@ -406,6 +406,99 @@ __global__ __launch_bounds__(256) void k_sorted_singular_values(SvtWs w, int B, 
     }
 }
 
+// ---- 5b'. U = Z - Z E on the bf16 matrix cores (B <= 224) -----------------------------------
+// Operands split exactly into three bf16 terms, six partial products (fp32-GEMM accuracy), so
+// the product leaves the VALU, which the concurrently running sparse-coding kernel saturates.
+// grid (row groups, column chunks of 64): each workgroup stages its 64 columns of E once (three
+// bf16 images [col][k], 464-B rows: conflict-free ds_read_b128) and loops over row blocks of 64;
+// wave w owns rows 16w..16w+15 of a block, 4 column tiles.
+typedef __bf16 sbf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kApKMax = 224, kApLd = 232, kApCols = 64;
+
+__device__ __forceinline__ void ap_split3(float v, __bf16 &a, __bf16 &b, __bf16 &c) {
+    a = (__bf16)v;
+    const float r1 = v - (float)a;
+    b = (__bf16)r1;
+    c = (__bf16)(r1 - (float)b);
+}
+
+__device__ __forceinline__ floatx4 ap_mfma(const sbf16x8 &a, const sbf16x8 &b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256) void k_svt_apply_b3(const float *__restrict__ X, const float *__restrict__ L2,
+                                                      float c2, const float *__restrict__ E, int64_t P, int B,
+                                                      float *__restrict__ U) {
+    extern __shared__ __align__(16) __bf16 Es[];   // [3][kApCols][kApLd]
+    const int c0 = blockIdx.y * kApCols;
+    for (int idx = threadIdx.x; idx < kApCols * kApKMax; idx += 256) {
+        const int cc = idx / kApKMax, k = idx % kApKMax;
+        const int c = c0 + cc;
+        const float v = (k < B && c < B) ? E[(int64_t)k * B + c] : 0.0f;
+        __bf16 a, b, d;
+        ap_split3(v, a, b, d);
+        Es[(0 * kApCols + cc) * kApLd + k] = a;
+        Es[(1 * kApCols + cc) * kApLd + k] = b;
+        Es[(2 * kApCols + cc) * kApLd + k] = d;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int jl = lane & 15, g = lane >> 4;
+    const int nks = (B + 31) / 32;
+    for (int64_t rb = (int64_t)blockIdx.x * 64; rb < P; rb += (int64_t)gridDim.x * 64) {
+        const int64_t row = rb + 16 * w + jl;            // A-operand row of this lane
+        floatx4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < nks; ++ks) {
+            const int kb = 32 * ks + 8 * g;
+            sbf16x8 A[3];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = kb + j;
+                float z = 0.0f;
+                if (row < P && k < B) {
+                    z = X[row * B + k];
+                    if (L2) z = z + c2 * L2[row * B + k];
+                }
+                __bf16 a, b, d;
+                ap_split3(z, a, b, d);
+                A[0][j] = a; A[1][j] = b; A[2][j] = d;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int cc = 16 * t + jl;
+                sbf16x8 Bf[3];
+#pragma unroll
+                for (int sp = 0; sp < 3; ++sp)
+                    Bf[sp] = *reinterpret_cast<const sbf16x8 *>(&Es[(sp * kApCols + cc) * kApLd + kb]);
+                floatx4 a4 = acc[t];
+                a4 = ap_mfma(A[2], Bf[0], a4);
+                a4 = ap_mfma(A[1], Bf[1], a4);
+                a4 = ap_mfma(A[0], Bf[2], a4);
+                a4 = ap_mfma(A[1], Bf[0], a4);
+                a4 = ap_mfma(A[0], Bf[1], a4);
+                a4 = ap_mfma(A[0], Bf[0], a4);
+                acc[t] = a4;
+            }
+        }
+        // C layout: rows 4g + i of the wave's 16, column jl of tile t
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int c = c0 + 16 * t + jl;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t r = rb + 16 * w + 4 * g + i;
+                if (r < P && c < B) {
+                    float z = X[r * B + c];
+                    if (L2) z = z + c2 * L2[r * B + c];
+                    U[r * B + c] = z - acc[t][i];
+                }
+            }
+        }
+    }
+}
+
 // ---- 5b. U = Z - Z E  (64 x 64 output tile per workgroup, f32) ------------------------------
 constexpr int kAT = 64;   // output tile
 constexpr int kAK = 16;   // k chunk
@@ -538,8 +631,19 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
         hipLaunchKernelGGL(k_sorted_singular_values, dim3(1), dim3(256), 0, st, w, (int)B, s_out);
         LRS_CHECK_LAUNCH();
     }
-    dim3 grid((unsigned)((P + kAT - 1) / kAT), (unsigned)((B + kAT - 1) / kAT));
-    hipLaunchKernelGGL(k_svt_apply, grid, dim3(256), 0, st, X, L2, c2, w.E, P, (int)B, U);
+    if (B <= kApKMax) {
+        const size_t lds = sizeof(__bf16) * 3 * kApCols * kApLd;
+        hipError_t e = hipFuncSetAttribute((const void *)k_svt_apply_b3, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e != hipSuccess) return (int)e;
+        int64_t rgroups = (P + 63) / 64;
+        if (rgroups > 64) rgroups = 64;
+        dim3 grid((unsigned)rgroups, (unsigned)((B + kApCols - 1) / kApCols));
+        hipLaunchKernelGGL(k_svt_apply_b3, grid, dim3(256), lds, st, X, L2, c2, w.E, P, (int)B, U);
+    } else {
+        dim3 grid((unsigned)((P + kAT - 1) / kAT), (unsigned)((B + kAT - 1) / kAT));
+        hipLaunchKernelGGL(k_svt_apply, grid, dim3(256), 0, st, X, L2, c2, w.E, P, (int)B, U);
+    }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }

@@ -1,5 +1,6 @@
 """Quality metrics of the reference (not timed): per-band PSNR with its 10*log10(255/RMSE)
-definition and the band mean (main_LRS_PnP.py:40-58, :379-384)."""
+definition and the band mean (main_LRS_PnP.py:40-58, :379-384), and MSSIM (pytorch_ssim.ssim,
+main_LRS_PnP_DIP_1-LiP.py:480-481) on the HIP kernel lrs_ssim_f32."""
 from __future__ import annotations
 
 import torch
@@ -20,3 +21,18 @@ def psnr_bands(X: torch.Tensor, clean_bhw: torch.Tensor) -> torch.Tensor:
 
 def mpsnr(X: torch.Tensor, clean_bhw: torch.Tensor) -> float:
     return float(psnr_bands(X, clean_bhw).mean())
+
+
+def mssim(img1: torch.Tensor, img2: torch.Tensor) -> float:
+    """pytorch_ssim.ssim(img1, img2) for (B, H, W) (or (1, B, H, W)) float32 device images."""
+    import ctypes
+
+    from ._lib import check, device_lib
+    a = img1.reshape(-1, *img1.shape[-2:]).contiguous().float()
+    b = img2.reshape(-1, *img2.shape[-2:]).contiguous().float()
+    C, H, W = a.shape
+    acc = torch.zeros(1, dtype=torch.float64, device=a.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    check(device_lib().lrs_ssim_f32(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), C, H, W,
+                                    ctypes.c_void_p(acc.data_ptr()), s), "lrs_ssim_f32")
+    return float(acc) / (C * H * W)

@@ -412,3 +412,24 @@ def test_solver_dip_pro_skip_runs(L, golden):
     assert torch.isfinite(s.X).all() and torch.isfinite(s.U).all()
     assert float(s.U.min()) >= 0.0 and float(s.U.max()) <= 1.0      # Sigmoid output
     assert s.dip_steps[0] == (40, None)
+
+
+def test_mssim_matches_torch_restatement(L):
+    """lrs_ssim_f32 vs the pytorch_ssim formula (pytorch_ssim/__init__.py:7-37) in torch fp64."""
+    import math
+    from lrspnp.metrics import mssim
+    g = torch.Generator().manual_seed(8)
+    a = torch.rand(7, 36, 29, generator=g)
+    b = (a + 0.1 * torch.randn(7, 36, 29, generator=g)).clamp(0, 1)
+    gauss = torch.tensor([math.exp(-(x - 5) ** 2 / float(2 * 1.5 ** 2)) for x in range(11)])
+    gauss = gauss / gauss.sum()
+    win = (gauss[:, None] @ gauss[None, :]).double().expand(7, 1, 11, 11)
+    A, Bt = a.double()[None], b.double()[None]
+    conv = lambda t: F.conv2d(t, win, padding=5, groups=7)
+    mu1, mu2 = conv(A), conv(Bt)
+    s1, s2, s12 = conv(A * A) - mu1 ** 2, conv(Bt * Bt) - mu2 ** 2, conv(A * Bt) - mu1 * mu2
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    ref = (((2 * mu1 * mu2 + C1) * (2 * s12 + C2)) / ((mu1 ** 2 + mu2 ** 2 + C1) * (s1 + s2 + C2))).mean()
+    got = mssim(a.cuda(), b.cuda())
+    assert abs(got - float(ref)) < 1e-5
+    assert abs(mssim(a.cuda(), a.cuda()) - 1.0) < 1e-6
