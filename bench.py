@@ -12,9 +12,11 @@ Multi-GPU (torchrun): one independent cube per rank (seed = rank), no data-path 
 value = (ranks * K) / max_time.
 
 Rank 0 prints one JSON line, including
-  roofline    : the dominant kernel (lrs_ista_f32 / k_ista) — algorithmic MFMA FLOPs per launch
-                (Nit*nb*4*n*K + nb*2*n*K) / mean launch time (HIP events on its stream), vs the
-                157.3 TFLOP/s fp32 MFMA peak; `traffic` from profiles/ PMC summary when present;
+  roofline    : the dominant kernel (lrs_ista_f32 / k_ista_b3) — algorithmic fp32-GEMM FLOPs per
+                launch (Nit*nb*4*n*K + nb*2*n*K) / mean launch time (HIP events on its stream), vs
+                the 157.3 TFLOP/s fp32 MFMA peak (the products are fp32-accurate split-bf16 MFMA;
+                the kernel itself is bound by the fp64 NLM VALU); `traffic` from
+                profiles/ PMC summary when present;
   cpu_baseline: the oracle (C restatement + numpy alpha/SVT, OpenMP) timed on a bounded sample
                 of the same workload on this host (N = 1, rank 0 only).
 """
@@ -262,7 +264,7 @@ def main():
         "config": {"workload": f"LRS-PnP (no DIP) {args.cube} cube, {args.bb}x{args.bb} blocks, K={K}, "
                                f"Nit={args.nit} inner ISTA, SVT low-rank prox (BASELINE configs[1])",
                    "blocks": nb, "parallelism": f"{world} independent cube(s), one per GPU"},
-        "roofline": {"bound": "mfma", "kernel": "k_ista (lrs_ista_f32)", "achieved": achieved,
+        "roofline": {"bound": "mfma", "kernel": "k_ista_b3 (lrs_ista_f32)", "achieved": achieved,
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                      "traffic": traffic, "flops_per_launch": flops, "ms_per_launch": ista_ms},
         "setup_s": setup_s,
