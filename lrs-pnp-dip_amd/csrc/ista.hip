@@ -52,6 +52,7 @@ struct IstaParams {
     float *phi;
     int n, n_pad, Nit, prox;
     int64_t nb;
+    double seven;   // 7.0, passed in so fma(7, x, c) keeps its addend in place (no per-use copy)
 };
 
 template <int K>
@@ -571,7 +572,7 @@ __device__ __forceinline__ void nlm_weights(const double (&w)[11], double kneg, 
 }
 
 __device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W1)[7], const int (&W2)[7],
-                                            const int (&W3)[7], double c0, float (&out)[4]) {
+                                            const int (&W3)[7], double c0, double seven, float (&out)[4]) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int C = 3 + e;
@@ -582,8 +583,8 @@ __device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W
 #pragma unroll
         for (int k = 0; k < 6; ++k) swv = __fma_rn(ws[k], vs[k], swv);   // canonical order
         const double sw = ((ws[0] + ws[5]) + (ws[1] + ws[4])) + (ws[2] + ws[3]);   // exact
-        const double num = __fma_rn(7.0, swv, c0 * w[C]);
-        const double den = __fma_rn(7.0, sw, c0);
+        const double num = __fma_rn(seven, swv, c0 * w[C]);
+        const double den = __fma_rn(seven, sw, c0);
         out[e] = nlm_div_fast(num, den);
     }
 }
@@ -594,7 +595,8 @@ __device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W
 template <int NQ, bool FULL>
 __device__ __forceinline__ void nlm_tile_reuse(int q, const NlmLanes &L, const float (&own)[4], const float (&Pprev)[3],
                                                const float (&Pcur)[3], const float (&Ncur)[4], const float (&Nnext)[4],
-                                               double kneg, double c0, Reuse6 &carry, float (&out)[4]) {
+                                               double kneg, double c0, double seven, Reuse6 &carry,
+                                               float (&out)[4]) {
     float prv[3], nxt[4];
     if (L.g == 0) {
         if (q == 0) { prv[0] = own[3]; prv[1] = own[2]; prv[2] = own[1]; }
@@ -626,7 +628,7 @@ __device__ __forceinline__ void nlm_tile_reuse(int q, const NlmLanes &L, const f
     carry.v[0] = W1[6];
     carry.v[1] = W2[5]; carry.v[2] = W2[6];
     carry.v[3] = W3[4]; carry.v[4] = W3[5]; carry.v[5] = W3[6];
-    nlm_outputs(w, W1, W2, W3, c0, out);
+    nlm_outputs(w, W1, W2, W3, c0, seven, out);
 }
 
 template <int K, bool SOFT>
@@ -732,9 +734,9 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) Nn[e] = __shfl(G[qb + 1][e], L.src_next, 64);
                 }
-                if (qa == 0) nlm_tile_reuse<NQ, true>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, carry, oa);
-                else nlm_tile_reuse<NQ, false>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, carry, oa);
-                nlm_tile_reuse<NQ, false>(qb, L, ownb, Pa, Pb, Nb, Nn, kneg, c0, carry, ob);
+                if (qa == 0) nlm_tile_reuse<NQ, true>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, p.seven, carry, oa);
+                else nlm_tile_reuse<NQ, false>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, p.seven, carry, oa);
+                nlm_tile_reuse<NQ, false>(qb, L, ownb, Pa, Pb, Nb, Nn, kneg, c0, p.seven, carry, ob);
 #pragma unroll
                 for (int e = 0; e < 3; ++e) Pprev[e] = Pb[e];
 #pragma unroll
@@ -951,7 +953,7 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     if (K != 256) return LRS_E_UNSUPPORTED;
     if (nb == 0) return LRS_OK;
     if (n_pad > (int64_t)1 << 20 || nb > ((int64_t)1 << 40)) return LRS_E_INVALID;
-    IstaParams p{Yb, obs, D, alpha, thr, coefs, phi, (int)n, (int)n_pad, Nit, prox, nb};
+    IstaParams p{Yb, obs, D, alpha, thr, coefs, phi, (int)n, (int)n_pad, Nit, prox, nb, 7.0};
     const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
     dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));
     hipStream_t st = (hipStream_t)stream;
@@ -989,7 +991,7 @@ extern "C" int lrs_diag_ista_ablate_f32(const float *Yb, const uint8_t *obs, con
                                         int64_t nb, const float *alpha, const double *thr, int Nit, int ablate,
                                         float *phi, void *stream) {
     if (n_pad > kStageRows || !phi) return LRS_E_INVALID;
-    IstaParams p{Yb, obs, D, alpha, thr, nullptr, phi, (int)n, (int)n_pad, Nit, LRS_PROX_NLM, nb};
+    IstaParams p{Yb, obs, D, alpha, thr, nullptr, phi, (int)n, (int)n_pad, Nit, LRS_PROX_NLM, nb, 7.0};
     const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
     dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));
     hipStream_t st = (hipStream_t)stream;
