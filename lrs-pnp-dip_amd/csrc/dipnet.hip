@@ -57,6 +57,8 @@ struct Split {
 
 // Tile choice and split-K: 128x128 tiles when they alone give >= 128 workgroups, else 64x64;
 // then split K until ~512 workgroups (2 per CU), keeping >= 128 of K per split and <= 64 splits.
+// (Measured: 128-tiles with deeper split-K on the small-N weight-gradient GEMMs, or a 1024-WG
+// target, are slower at both the 36x36 and the 196x196 sizes.)
 Split choose_split(int M, int N, int K) {
     const int64_t t128 = (int64_t)((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
     const bool big = t128 >= 128;
@@ -703,13 +705,15 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
         } else {
             return fail(LRS_E_INVALID);
         }
+        // BN partials: every BN and every conv (its bias gradient is reduced the same way)
+        if ((N.d.bn || N.d.kind == LRS_NODE_CONV) && bn_part_doubles(N.C, N.P) > max_bnpart)
+            max_bnpart = bn_part_doubles(N.C, N.P);
         if (N.d.bn) {
             N.gm_off = pofs; pofs += N.C;
             N.bt_off = pofs; pofs += N.C;
             N.rs_off = rofs; rofs += 2 * N.C;
             N.mean_off = ofs; ofs += align64(N.C);
             N.istd_off = ofs; ofs += align64(N.C);
-            if (bn_part_doubles(N.C, N.P) > max_bnpart) max_bnpart = bn_part_doubles(N.C, N.P);
         } else if (N.d.kind == LRS_NODE_CONV) {
             N.mean_off = ofs; ofs += align64(N.C);   // unused placeholders (the kernels take them)
             N.istd_off = ofs; ofs += align64(N.C);

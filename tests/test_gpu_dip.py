@@ -289,6 +289,17 @@ def test_unet_generalised_bands_196(L):
     out = net.forward(x.cuda()).cpu()
     assert out.shape == (198, 196, 196)
     assert rel(out, dip_ref.forward(flat, units, x)) < 1e-5
+    # training steps at this size (the last conv has 198 > 128 channels and no BN: its bias-gradient
+    # partials must fit the workspace) — loss of the first step = the restatement's
+    t = torch.rand(198, 196, 196, generator=g)
+    m = (torch.rand(196 * 196, generator=g) > 0.2).float()
+    loss_ref = float(dip_ref.loss_fn(dip_ref.forward(flat, units, x), t, m))
+    net.train_steps(x.cuda(), t.cuda(), m.cuda(), 1, use_graph=False)
+    torch.cuda.synchronize()
+    assert abs(net.last_loss() - loss_ref) < 1e-5 * loss_ref
+    net.train_steps(x.cuda(), t.cuda(), m.cuda(), 2, use_graph=False)
+    assert np.isfinite(net.last_loss()) and net.last_loss() > 0
+    assert torch.isfinite(net.params).all()
 
 
 def test_lipschitz_dip_run_early_stop(L):

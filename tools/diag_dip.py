@@ -14,7 +14,7 @@ from lrspnp.dip import DipNet, lipschitz_unet_units  # noqa: E402
 
 
 def run(bands, H, steps, graph):
-    net = DipNet(lipschitz_unet_units(bands, bands, 128), H, H)
+    net = DipNet(lipschitz_unet_units(bands, bands, 128), bands, H, H)
     net.init_params(1)
     g = torch.Generator(device="cuda").manual_seed(0)
     x = torch.rand(bands, H, H, device="cuda", generator=g)
