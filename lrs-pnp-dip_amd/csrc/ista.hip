@@ -429,9 +429,9 @@ __device__ __forceinline__ void split3(float v, __bf16 &a, __bf16 &b, __bf16 &c)
 constexpr int kB3Waves = 4;                       // one wave per SIMD: the whole 512-entry register file
 constexpr int kB3Threads = kB3Waves * kWave;
 
-template <int K>
+template <int K, int THREADS>
 __device__ __forceinline__ void stage_dictionary_b3(IstaSmemB3<K> &S, const float *__restrict__ D, int n) {
-    for (int idx = threadIdx.x; idx < kStageRows * K; idx += kB3Threads) {
+    for (int idx = threadIdx.x; idx < kStageRows * K; idx += THREADS) {
         const int r = idx / K, a = idx % K;
         const float v = r < n ? D[(int64_t)r * K + a] : 0.0f;
         __bf16 h, m, l;
@@ -522,6 +522,11 @@ __device__ __forceinline__ void b3_gemm1(const IstaSmemB3<K> &S, int p, const bf
 // are exact in fp64 (<= 6 terms of 21 significant bits within 8 binades), so their order is free;
 // num/den uses one Newton step on v_rcp_f64 and a remainder correction (|error| < 1 ulp of fp64
 // before the final float rounding, instead of the IEEE division sequence).
+template <int ABL>
+__device__ __forceinline__ int shf(int v, int src) { return ABL == 1 ? v : __shfl(v, src, 64); }
+template <int ABL>
+__device__ __forceinline__ float shf(float v, int src) { return ABL == 1 ? v : __shfl(v, src, 64); }
+
 struct Reuse6 {
     int v[6];   // W1[6], W2[5], W2[6], W3[4], W3[5], W3[6] of a chunk
 };
@@ -592,7 +597,7 @@ __device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W
 // tile q of the NLM with weight reuse (FULL for the first tile, whose g == 0 chunk has a
 // reflected window).  `carry`: this lane's trailing weights of tile q-1 on entry, of tile q on
 // exit; only the g == 3 lanes' copy is read (by the g == 0 lanes of the next tile).
-template <int NQ, bool FULL>
+template <int NQ, bool FULL, int ABL = 0>
 __device__ __forceinline__ void nlm_tile_reuse(int q, const NlmLanes &L, const float (&own)[4], const float (&Pprev)[3],
                                                const float (&Pcur)[3], const float (&Ncur)[4], const float (&Nnext)[4],
                                                double kneg, double c0, double seven, Reuse6 &carry,
@@ -620,7 +625,7 @@ __device__ __forceinline__ void nlm_tile_reuse(int q, const NlmLanes &L, const f
         const int mine[6] = {W1[6], W2[5], W2[6], W3[4], W3[5], W3[6]};
         int prev[6];
 #pragma unroll
-        for (int e = 0; e < 6; ++e) prev[e] = __shfl((L.g == 3) ? carry.v[e] : mine[e], L.src_prev, 64);
+        for (int e = 0; e < 6; ++e) prev[e] = shf<ABL>((L.g == 3) ? carry.v[e] : mine[e], L.src_prev);
         W1[2] = prev[0];
         W2[1] = prev[1]; W2[2] = prev[2];
         W3[0] = prev[3]; W3[1] = prev[4]; W3[2] = prev[5];
@@ -631,15 +636,32 @@ __device__ __forceinline__ void nlm_tile_reuse(int q, const NlmLanes &L, const f
     nlm_outputs(w, W1, W2, W3, c0, seven, out);
 }
 
-template <int K, bool SOFT>
-__global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
+// sched_group_barrier pattern for one pipeline step with NM MFMAs (groups of 6 sharing 6 LDS reads,
+// the reads one group ahead) and V VALU instructions after each MFMA
+template <int NM, int V>
+__device__ __forceinline__ void b3_interleave() {
+    constexpr int NG = NM / 6;
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+        if (gi + 1 < NG) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, V, 0);
+        }
+    }
+}
+
+template <int K, bool SOFT, int WAVES = kB3Waves, bool SEQ = false, int ABL = 0, int PIPE = 0>
+__global__ __launch_bounds__(WAVES * kWave, 1) void k_ista_b3(IstaParams p) {
     static_assert(K == 256, "the chunk swizzle assumes 64 chunks per row");
     constexpr int NQ = K / 16;
     __shared__ __attribute__((aligned(16))) IstaSmemB3<K> S;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int jl = lane & 15, g = lane >> 4;
-    const int64_t j = ((int64_t)blockIdx.x * kB3Waves + wave) * 16 + jl;
+    const int64_t j = ((int64_t)blockIdx.x * WAVES + wave) * 16 + jl;
     const bool valid = j < p.nb;
     const int NT = p.n_pad / 16;
     const NlmLanes L(lane);
@@ -664,7 +686,7 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) mres |= (((mv >> (8 * i)) & 0xffu) ? 1u : 0u) << (4 * t + i);
     }
-    stage_dictionary_b3<K>(S, p.D, p.n);
+    stage_dictionary_b3<K, WAVES * kWave>(S, p.D, p.n);
     __syncthreads();
 
     float X[NQ][4];
@@ -694,20 +716,29 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
         // pipeline over tile pairs: step p runs the products of tiles 2p+4, 2p+5 and the
         // (independent, so interleavable) NLM of tiles 2p and 2p+1 on one wave's instruction stream
         floatx4 G[NQ];
+        auto gemm2q = [&](int q) -> floatx4 {
+            if (ABL == 3) return floatx4{r[0][0] + q, r[1][1], r[2][2], r[3][3]};
+            return b3_gemm2<K>(S, q, rf, lane);
+        };
 #pragma unroll
-        for (int q = 0; q < 4; ++q) G[q] = b3_gemm2<K>(S, q, rf, lane);
+        for (int q = 0; q < 4; ++q) G[q] = gemm2q(q);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) gradient(G[q], X[q]);
         float Pprev[3] = {0.f, 0.f, 0.f}, Ncur[4];
         Reuse6 carry{};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Ncur[e] = __shfl(G[0][e], L.src_next, 64);
+        for (int e = 0; e < 4; ++e) Ncur[e] = shf<ABL>(G[0][e], L.src_next);
 #pragma unroll
         for (int pp = 0; pp < NQ / 2; ++pp) {
             const int qa = 2 * pp, qb = qa + 1;
-            if (qa + 4 < NQ) G[qa + 4] = b3_gemm2<K>(S, qa + 4, rf, lane);
-            if (qb + 4 < NQ) G[qb + 4] = b3_gemm2<K>(S, qb + 4, rf, lane);
+            if (qa + 4 < NQ) G[qa + 4] = gemm2q(qa + 4);
+            if (qb + 4 < NQ) G[qb + 4] = gemm2q(qb + 4);
+            if (PIPE && pp > 0) {   // D x of the previous pair beside this pair's NLM
+                bf16x8 xf[3];
+                split_frag(X[qa - 2], X[qb - 2], xf);
+                b3_gemm1<K>(S, pp - 1, xf, R, lane);
+            }
             float oa[4], ob[4];
             if (SOFT) {
 #pragma unroll
@@ -719,24 +750,28 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
                     u = u > 0.f ? u : 0.f;
                     ob[i] = G[qb][i] > 0.f ? u : (G[qb][i] < 0.f ? -u : 0.f);
                 }
+            } else if (ABL == 2) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { oa[i] = G[qa][i]; ob[i] = G[qb][i]; }
             } else {
                 const float owna[4] = {G[qa][0], G[qa][1], G[qa][2], G[qa][3]};
                 const float ownb[4] = {G[qb][0], G[qb][1], G[qb][2], G[qb][3]};
                 float Pa[3], Pb[3], Nb[4], Nn[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int e = 0; e < 3; ++e) {
-                    Pa[e] = __shfl(G[qa][e + 1], L.src_prev, 64);
-                    Pb[e] = __shfl(G[qb][e + 1], L.src_prev, 64);
+                    Pa[e] = shf<ABL>(G[qa][e + 1], L.src_prev);
+                    Pb[e] = shf<ABL>(G[qb][e + 1], L.src_prev);
                 }
 #pragma unroll
-                for (int e = 0; e < 4; ++e) Nb[e] = __shfl(G[qb][e], L.src_next, 64);
+                for (int e = 0; e < 4; ++e) Nb[e] = shf<ABL>(G[qb][e], L.src_next);
                 if (qb + 1 < NQ) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) Nn[e] = __shfl(G[qb + 1][e], L.src_next, 64);
+                    for (int e = 0; e < 4; ++e) Nn[e] = shf<ABL>(G[qb + 1][e], L.src_next);
                 }
-                if (qa == 0) nlm_tile_reuse<NQ, true>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, p.seven, carry, oa);
-                else nlm_tile_reuse<NQ, false>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, p.seven, carry, oa);
-                nlm_tile_reuse<NQ, false>(qb, L, ownb, Pa, Pb, Nb, Nn, kneg, c0, p.seven, carry, ob);
+                if (qa == 0) nlm_tile_reuse<NQ, true, ABL>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, p.seven, carry, oa);
+                else nlm_tile_reuse<NQ, false, ABL>(qa, L, owna, Pprev, Pa, Ncur, Nb, kneg, c0, p.seven, carry, oa);
+                if (SEQ) __builtin_amdgcn_sched_barrier(0);
+                nlm_tile_reuse<NQ, false, ABL>(qb, L, ownb, Pa, Pb, Nb, Nn, kneg, c0, p.seven, carry, ob);
 #pragma unroll
                 for (int e = 0; e < 3; ++e) Pprev[e] = Pb[e];
 #pragma unroll
@@ -744,14 +779,28 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) { X[qa][i] = oa[i]; X[qb][i] = ob[i]; }
-            {
+            if (!PIPE) {
                 bf16x8 xf[3];
                 split_frag(X[qa], X[qb], xf);
-                b3_gemm1<K>(S, pp, xf, R, lane);
+                if (ABL == 3) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) R[t][t] += X[qa][t] * X[qb][3 - t];
+                } else {
+                    b3_gemm1<K>(S, pp, xf, R, lane);
+                }
             }
             if (qa + 4 < NQ) gradient(G[qa + 4], X[qa + 4]);
             if (qb + 4 < NQ) gradient(G[qb + 4], X[qb + 4]);
+            if (PIPE == 2) {
+                if (pp > 0 && qa + 4 < NQ) b3_interleave<48, 12>();
+                else b3_interleave<24, 24>();
+            }
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if (PIPE) {
+            bf16x8 xf[3];
+            split_frag(X[NQ - 2], X[NQ - 1], xf);
+            b3_gemm1<K>(S, NQ / 2 - 1, xf, R, lane);
         }
     }
 
@@ -760,6 +809,579 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_b3(IstaParams p) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q)
                 *reinterpret_cast<float4 *>(&p.coefs[j * K + 16 * q + 4 * g]) =
+                    make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t < NT)
+                *reinterpret_cast<float4 *>(&p.phi[j * p.n_pad + 16 * t + 4 * g]) =
+                    make_float4(R[t][0], R[t][1], R[t][2], R[t][3]);
+    }
+}
+
+// ---- split-bf16 kernel, lane-contiguous atom layout ----------------------------------------------
+// The atom order inside the MFMA tiles is free (it is the A operand's row choice), so tile q row
+// 4g+i holds atom 64g + 4q + i: lane group g owns the 64 consecutive atoms 64g .. 64g+63 across its
+// 16 tiles.  The NLM neighbours of a chunk are then the lane's own previous / next tile, except at
+// the group edges (tile 0's left and tile 15's right neighbours: 7 shuffles per iteration instead
+// of ~200), and the 6 reused weights of each chunk are the lane's own previous chunk's.
+// LDS image: split s of D at [row][atom], 4-atom chunk c stored at pi(c) ^ (row & 15) with
+// pi(c) = c ^ 8 (c >= 32): conflict-free for both the gemm2 transposed reads (chunks 16p + q)
+// and the gemm1 row reads (chunks 16g + 2p, +1) — exhaustively checked per 32-lane half.
+template <int K>
+__device__ __forceinline__ int ln_off(int row, int chunk) {
+    const int pc = chunk ^ (((chunk >> 5) & 1) << 3);
+    return row * K + 4 * (pc ^ (row & 15));
+}
+
+template <int K, int THREADS>
+__device__ __forceinline__ void stage_dictionary_ln(IstaSmemB3<K> &S, const float *__restrict__ D, int n) {
+    for (int idx = threadIdx.x; idx < kStageRows * K; idx += THREADS) {
+        const int r = idx / K, a = idx % K;
+        const float v = r < n ? D[(int64_t)r * K + a] : 0.0f;
+        __bf16 h, m, l;
+        split3(v, h, m, l);
+        const int o = ln_off<K>(r, a >> 2) + (a & 3);
+        S.D[0][0][o] = h;
+        S.D[1][0][o] = m;
+        S.D[2][0][o] = l;
+    }
+}
+
+// G tile q = D^T r with tile row 4g+i = atom 64g + 4q + i
+template <int K>
+__device__ __forceinline__ floatx4 ln_gemm2(const IstaSmemB3<K> &S, int q, const bf16x8 (&rf)[2][3], int lane) {
+    const int g = lane >> 4, ll = lane & 15, qq = ll >> 2, pp = ll & 3;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+        const int r0 = 32 * pr + 4 * g + qq, r1 = r0 + 16;
+        bf16x8 A[3];
+#pragma unroll
+        for (int sp = 0; sp < 3; ++sp) {
+            typedef __attribute__((address_space(3))) short4v lds_s4;
+            const short4v a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s4 *)(&S.D[sp][0][ln_off<K>(r0, 16 * pp + q)]));
+            const short4v a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s4 *)(&S.D[sp][0][ln_off<K>(r1, 16 * pp + q)]));
+            A[sp] = cat4(__builtin_bit_cast(bf16x4, a0), __builtin_bit_cast(bf16x4, a1));
+        }
+        acc = mfma_split6(A, rf[pr], acc);
+    }
+    return acc;
+}
+
+// R[t] += D rows (16t..) x the lane's atoms 64g + 8p .. 64g + 8p + 7 (tiles 2p, 2p+1)
+template <int K>
+__device__ __forceinline__ void ln_gemm1(const IstaSmemB3<K> &S, int p, const bf16x8 (&xf)[3], floatx4 (&R)[4],
+                                         int lane) {
+    const int g = lane >> 4, ll = lane & 15;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int row = 16 * t + ll;
+        bf16x8 A[3];
+#pragma unroll
+        for (int sp = 0; sp < 3; ++sp) {
+            const bf16x4 a0 = *reinterpret_cast<const bf16x4 *>(&S.D[sp][0][ln_off<K>(row, 16 * g + 2 * p)]);
+            const bf16x4 a1 = *reinterpret_cast<const bf16x4 *>(&S.D[sp][0][ln_off<K>(row, 16 * g + 2 * p + 1)]);
+            A[sp] = cat4(a0, a1);
+        }
+        R[t] = mfma_split6(A, xf, R[t]);
+    }
+}
+
+// NLM of one 4-atom chunk from its 3 left / 4 right neighbours; `carry` = the previous chunk's
+// trailing weights on entry (unused when FULL), this chunk's on exit
+template <bool FULL>
+__device__ __forceinline__ void nlm_chunk_ln(const float (&prv)[3], const floatx4 &own, const float (&nxt)[4],
+                                             double kneg, double c0, double seven, int (&carry)[6],
+                                             float (&out)[4]) {
+    const double w[11] = {prv[0], prv[1], prv[2], own[0], own[1], own[2], own[3],
+                          nxt[0], nxt[1], nxt[2], nxt[3]};
+    int W1[7], W2[7], W3[7];
+    nlm_weights<FULL>(w, kneg, W1, W2, W3);
+    if (!FULL) {
+        W1[2] = carry[0];
+        W2[1] = carry[1]; W2[2] = carry[2];
+        W3[0] = carry[3]; W3[1] = carry[4]; W3[2] = carry[5];
+    }
+    carry[0] = W1[6];
+    carry[1] = W2[5]; carry[2] = W2[6];
+    carry[3] = W3[4]; carry[4] = W3[5]; carry[5] = W3[6];
+    nlm_outputs(w, W1, W2, W3, c0, seven, out);
+}
+
+template <int K, bool SOFT, int LA = 2, int EXP = 0>
+__global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln(IstaParams p) {
+    static_assert(K == 256, "the lane layout assumes 4 groups of 64 atoms");
+    constexpr int NQ = K / 16;
+    __shared__ __attribute__((aligned(16))) IstaSmemB3<K> S;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int jl = lane & 15, g = lane >> 4;
+    const int64_t j = ((int64_t)blockIdx.x * kB3Waves + wave) * 16 + jl;
+    const bool valid = j < p.nb;
+    const int NT = p.n_pad / 16;
+    const int src_prev = (lane + 48) & 63, src_next = (lane + 16) & 63;
+
+    const float alpha = valid ? p.alpha[j] : 1.0f;
+    const double thr = valid ? p.thr[j] : 1.0;
+    const double kneg = nlm_kneg(thr);
+    const double c0 = nlm_c0();
+    const float Tsoft = (float)thr;
+
+    float y[4][4];
+    uint32_t mres = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        float4 yv = {0.f, 0.f, 0.f, 0.f};
+        uint32_t mv = 0;
+        if (valid && t < NT) {
+            yv = *reinterpret_cast<const float4 *>(&p.Yb[j * p.n_pad + 16 * t + 4 * g]);
+            mv = *reinterpret_cast<const uint32_t *>(&p.obs[j * p.n_pad + 16 * t + 4 * g]);
+        }
+        y[t][0] = yv.x; y[t][1] = yv.y; y[t][2] = yv.z; y[t][3] = yv.w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mres |= (((mv >> (8 * i)) & 0xffu) ? 1u : 0u) << (4 * t + i);
+    }
+    stage_dictionary_ln<K, kB3Threads>(S, p.D, p.n);
+    __syncthreads();
+
+    float X[NQ][4];   // X[q][i] = coefficient of atom 64g + 4q + i
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) X[q][0] = X[q][1] = X[q][2] = X[q][3] = 0.f;
+    floatx4 R[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const float ainv = 1.0f / alpha;
+    auto gradient = [&](floatx4 &Gq, const float (&xq)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Gq[i] = xq[i] + div_by(Gq[i], alpha, ainv);
+    };
+    auto soft = [&](const floatx4 &Gq, float (&o)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float t = fabsf(Gq[i]) - Tsoft;
+            t = t > 0.f ? t : 0.f;
+            o[i] = Gq[i] > 0.f ? t : (Gq[i] < 0.f ? -t : 0.f);
+        }
+    };
+
+    for (int it = 0; it < p.Nit; ++it) {
+        float r[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[t][i] = ((mres >> (4 * t + i)) & 1u) ? (y[t][i] - R[t][i]) : 0.0f;
+            R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        bf16x8 rf[2][3];
+        split_frag(r[0], r[1], rf[0]);
+        split_frag(r[2], r[3], rf[1]);
+        // prologue: tile 15 (whose last atoms are the next group's left neighbours) and tiles 0..3;
+        // step p then runs the products of tiles 2p+4, 2p+5 (<= 14) and the D x of pair p-1 beside
+        // the NLM of tiles 2p, 2p+1
+        floatx4 G[NQ];
+        constexpr int QL = NQ;   // tile 15 is recomputed in the pipeline (its early copy only feeds the edge)
+#pragma unroll
+        for (int q = 0; q < 2 * LA; ++q) G[q] = ln_gemm2<K>(S, q, rf, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 2 * LA; ++q) gradient(G[q], X[q]);
+        float edge_prev[3], edge_next[4];
+        if (!SOFT) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) edge_next[e] = __shfl(G[0][e], src_next, 64);
+        }
+        int carry[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int pp = 0; pp < NQ / 2; ++pp) {
+            const int qa = 2 * pp, qb = qa + 1;
+            if (qa + 2 * LA < QL) G[qa + 2 * LA] = ln_gemm2<K>(S, qa + 2 * LA, rf, lane);
+            if (qb + 2 * LA < QL) G[qb + 2 * LA] = ln_gemm2<K>(S, qb + 2 * LA, rf, lane);
+            if (pp == 0) {  // tile 15's last atoms are the next group's left neighbours
+                floatx4 G15 = ln_gemm2<K>(S, NQ - 1, rf, lane);
+                gradient(G15, X[NQ - 1]);
+                if (!SOFT) {
+#pragma unroll
+                    for (int e = 0; e < 3; ++e) {
+                        const float v = __shfl(G15[e + 1], src_prev, 64);
+                        edge_prev[e] = (g == 0) ? G[0][3 - e] : v;      // reflect: atoms -3,-2,-1 -> 3,2,1
+                    }
+                }
+            }
+            if (pp > 0) {   // D x of the previous pair beside this pair's NLM
+                bf16x8 xf[3];
+                split_frag(X[qa - 2], X[qb - 2], xf);
+                ln_gemm1<K>(S, pp - 1, xf, R, lane);
+            }
+            float oa[4], ob[4];
+            if (SOFT) {
+                soft(G[qa], oa);
+                soft(G[qb], ob);
+            } else {
+                float prv[3], nxt[4];
+                if (qa == 0) {
+#pragma unroll
+                    for (int e = 0; e < 3; ++e) prv[e] = edge_prev[e];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 3; ++e) prv[e] = G[qa - 1][e + 1];
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) nxt[e] = G[qb][e];
+                if (qa == 0 || (EXP & 2)) nlm_chunk_ln<true>(prv, G[qa], nxt, kneg, c0, p.seven, carry, oa);
+                else nlm_chunk_ln<false>(prv, G[qa], nxt, kneg, c0, p.seven, carry, oa);
+                if (EXP & 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int e = 0; e < 3; ++e) prv[e] = G[qa][e + 1];
+                if (qb == NQ - 1) {    // reflect: atoms 256..259 -> 254, 253, 252, 251
+                    const float rfl[4] = {G[qb][2], G[qb][1], G[qb][0], G[qa][3]};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) nxt[e] = (g == 3) ? rfl[e] : edge_next[e];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) nxt[e] = G[qb + 1][e];
+                }
+                if (EXP & 2) nlm_chunk_ln<true>(prv, G[qb], nxt, kneg, c0, p.seven, carry, ob);
+                else nlm_chunk_ln<false>(prv, G[qb], nxt, kneg, c0, p.seven, carry, ob);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { X[qa][i] = oa[i]; X[qb][i] = ob[i]; }
+            if (qa + 2 * LA < QL) gradient(G[qa + 2 * LA], X[qa + 2 * LA]);
+            if (qb + 2 * LA < QL) gradient(G[qb + 2 * LA], X[qb + 2 * LA]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        {
+            bf16x8 xf[3];
+            split_frag(X[NQ - 2], X[NQ - 1], xf);
+            ln_gemm1<K>(S, NQ / 2 - 1, xf, R, lane);
+        }
+    }
+
+    if (valid) {
+        if (p.coefs) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                *reinterpret_cast<float4 *>(&p.coefs[j * K + 64 * g + 4 * q]) =
+                    make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t < NT)
+                *reinterpret_cast<float4 *>(&p.phi[j * p.n_pad + 16 * t + 4 * g]) =
+                    make_float4(R[t][0], R[t][1], R[t][2], R[t][3]);
+    }
+}
+
+// ---- explicitly scheduled lane-layout kernel -------------------------------------------------------
+// Per iteration: prologue (residual, tiles 0..3 and the edge copy of tile 15), then 8 steps of 4
+// slots.  Slot k of step p runs one NLM phase (weights / outputs of chunk 2p, then of 2p+1) beside
+// the MFMAs of up to two 6-MFMA units (a gemm2 tile half or a gemm1 row tile) whose LDS operands
+// the previous slot loaded, and loads the next slot's operands.
+struct Frag3 {
+    bf16x8 a[3];
+};
+
+// Tile-major image (LAY 1): chunk c = 16 p' + q' of row r at element q' * 1024 + r * 16 + 4 (p' ^ s(r)),
+// s(r) = 2 ((r >> 3) & 1).  Every read of a tile / row tile is a lane-constant base plus an
+// immediate (no per-read address VALU), and both read kinds are conflict-free per 32-lane half.
+__device__ __forceinline__ int tm_off(int row, int chunk) {
+    return (chunk & 15) * 1024 + row * 16 + 4 * ((chunk >> 4) ^ (((row >> 3) & 1) << 1));
+}
+
+template <int K, int THREADS>
+__device__ __forceinline__ void stage_dictionary_tm(IstaSmemB3<K> &S, const float *__restrict__ D, int n) {
+    for (int idx = threadIdx.x; idx < kStageRows * K; idx += THREADS) {
+        const int r = idx / K, a = idx % K;
+        const float v = r < n ? D[(int64_t)r * K + a] : 0.0f;
+        __bf16 h, m, l;
+        split3(v, h, m, l);
+        const int o = tm_off(r, a >> 2) + (a & 3);
+        S.D[0][0][o] = h;
+        S.D[1][0][o] = m;
+        S.D[2][0][o] = l;
+    }
+}
+
+struct TmLane {
+    int tr, g1;   // lane-constant element offsets of the transposed and the row reads
+    __device__ __forceinline__ explicit TmLane(int lane) {
+        const int g = lane >> 4, ll = lane & 15, qq = ll >> 2, pp = ll & 3, rt = 4 * g + qq;
+        tr = rt * 16 + 4 * (pp ^ (((rt >> 3) & 1) << 1));
+        g1 = ll * 16 + 4 * (g ^ (((ll >> 3) & 1) << 1));
+    }
+};
+
+template <int K>
+__device__ __forceinline__ void tm_load_g2(const IstaSmemB3<K> &S, int q, int pr, const TmLane &A, Frag3 &F) {
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) {
+        typedef __attribute__((address_space(3))) short4v lds_s4;
+        const __bf16 *b = &S.D[sp][0][0] + A.tr + q * 1024 + pr * 512;
+        const short4v a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)b);
+        const short4v a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(b + 256));
+        F.a[sp] = cat4(__builtin_bit_cast(bf16x4, a0), __builtin_bit_cast(bf16x4, a1));
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void tm_load_g1(const IstaSmemB3<K> &S, int t, int p, const TmLane &A, Frag3 &F) {
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) {
+        const __bf16 *b = &S.D[sp][0][0] + A.g1 + 2 * p * 1024 + t * 256;
+        const bf16x4 a0 = *reinterpret_cast<const bf16x4 *>(b);
+        const bf16x4 a1 = *reinterpret_cast<const bf16x4 *>(b + 1024);
+        F.a[sp] = cat4(a0, a1);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void ln_load_g2(const IstaSmemB3<K> &S, int q, int pr, int lane, Frag3 &F) {
+    const int g = lane >> 4, ll = lane & 15, qq = ll >> 2, pp = ll & 3;
+    const int r0 = 32 * pr + 4 * g + qq, r1 = r0 + 16;
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) {
+        typedef __attribute__((address_space(3))) short4v lds_s4;
+        const short4v a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(&S.D[sp][0][ln_off<K>(r0, 16 * pp + q)]));
+        const short4v a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(&S.D[sp][0][ln_off<K>(r1, 16 * pp + q)]));
+        F.a[sp] = cat4(__builtin_bit_cast(bf16x4, a0), __builtin_bit_cast(bf16x4, a1));
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void ln_load_g1(const IstaSmemB3<K> &S, int t, int p, int lane, Frag3 &F) {
+    const int g = lane >> 4, ll = lane & 15, row = 16 * t + ll;
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) {
+        const bf16x4 a0 = *reinterpret_cast<const bf16x4 *>(&S.D[sp][0][ln_off<K>(row, 16 * g + 2 * p)]);
+        const bf16x4 a1 = *reinterpret_cast<const bf16x4 *>(&S.D[sp][0][ln_off<K>(row, 16 * g + 2 * p + 1)]);
+        F.a[sp] = cat4(a0, a1);
+    }
+}
+
+// unit u (0/1) of slot k of step pp: kind 0 none, 1 gemm2 (tile a, half b), 2 gemm1 (row tile a, pair b)
+struct LnUnit {
+    int kind, a, b;
+};
+__device__ constexpr LnUnit ln_unit(int pp, int k, int u) {
+    if (pp < 0 || pp > 7) return {0, 0, 0};
+    if (pp == 0) return u == 0 ? LnUnit{1, 4 + (k >> 1), k & 1} : LnUnit{0, 0, 0};
+    if (pp >= 6) return u == 0 ? LnUnit{2, k, pp - 1} : LnUnit{0, 0, 0};
+    const int idx = 2 * k + u;      // 0..3 gemm2 halves of tiles 2pp+4, 2pp+5; 4..7 gemm1 row tiles
+    if (idx < 4) return {1, 2 * pp + 4 + (idx >> 1), idx & 1};
+    return {2, idx - 4, pp - 1};
+}
+
+template <int K, int LAY>
+__device__ __forceinline__ void ln_load_unit(const IstaSmemB3<K> &S, LnUnit U, int lane, const TmLane &A, Frag3 &F) {
+    if (LAY == 1) {
+        if (U.kind == 1) tm_load_g2<K>(S, U.a, U.b, A, F);
+        else if (U.kind == 2) tm_load_g1<K>(S, U.a, U.b, A, F);
+    } else {
+        if (U.kind == 1) ln_load_g2<K>(S, U.a, U.b, lane, F);
+        else if (U.kind == 2) ln_load_g1<K>(S, U.a, U.b, lane, F);
+    }
+}
+
+// whole-tile products through the unit loaders (prologue / epilogue)
+template <int K, int LAY>
+__device__ __forceinline__ floatx4 lay_gemm2(const IstaSmemB3<K> &S, int q, const bf16x8 (&rf)[2][3], int lane,
+                                             const TmLane &A) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+        Frag3 F;
+        ln_load_unit<K, LAY>(S, LnUnit{1, q, pr}, lane, A, F);
+        acc = mfma_split6(F.a, rf[pr], acc);
+    }
+    return acc;
+}
+
+template <int K, int LAY>
+__device__ __forceinline__ void lay_gemm1(const IstaSmemB3<K> &S, int p, const bf16x8 (&xf)[3], floatx4 (&R)[4],
+                                          int lane, const TmLane &A) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        Frag3 F;
+        ln_load_unit<K, LAY>(S, LnUnit{2, t, p}, lane, A, F);
+        R[t] = mfma_split6(F.a, xf, R[t]);
+    }
+}
+
+template <int K, bool GB, int LAY = 0>
+__global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln2(IstaParams p) {
+    static_assert(K == 256, "the lane layout assumes 4 groups of 64 atoms");
+    constexpr int NQ = K / 16;
+    __shared__ __attribute__((aligned(16))) IstaSmemB3<K> S;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int jl = lane & 15, g = lane >> 4;
+    const int64_t j = ((int64_t)blockIdx.x * kB3Waves + wave) * 16 + jl;
+    const bool valid = j < p.nb;
+    const int NT = p.n_pad / 16;
+    const int src_prev = (lane + 48) & 63, src_next = (lane + 16) & 63;
+    const TmLane AL(lane);
+
+    const float alpha = valid ? p.alpha[j] : 1.0f;
+    const double thr = valid ? p.thr[j] : 1.0;
+    const double kneg = nlm_kneg(thr);
+    const double c0 = nlm_c0();
+
+    float y[4][4];
+    uint32_t mres = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        float4 yv = {0.f, 0.f, 0.f, 0.f};
+        uint32_t mv = 0;
+        if (valid && t < NT) {
+            yv = *reinterpret_cast<const float4 *>(&p.Yb[j * p.n_pad + 16 * t + 4 * g]);
+            mv = *reinterpret_cast<const uint32_t *>(&p.obs[j * p.n_pad + 16 * t + 4 * g]);
+        }
+        y[t][0] = yv.x; y[t][1] = yv.y; y[t][2] = yv.z; y[t][3] = yv.w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mres |= (((mv >> (8 * i)) & 0xffu) ? 1u : 0u) << (4 * t + i);
+    }
+    if (LAY == 1) stage_dictionary_tm<K, kB3Threads>(S, p.D, p.n);
+    else stage_dictionary_ln<K, kB3Threads>(S, p.D, p.n);
+    __syncthreads();
+
+    float X[NQ][4];   // X[q][i] = coefficient of atom 64g + 4q + i
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) X[q][0] = X[q][1] = X[q][2] = X[q][3] = 0.f;
+    floatx4 R[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const float ainv = 1.0f / alpha;
+    auto gradient = [&](floatx4 &Gq, const float (&xq)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Gq[i] = xq[i] + div_by(Gq[i], alpha, ainv);
+    };
+
+    for (int it = 0; it < p.Nit; ++it) {
+        float r[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[t][i] = ((mres >> (4 * t + i)) & 1u) ? (y[t][i] - R[t][i]) : 0.0f;
+            R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        bf16x8 rf[2][3];
+        split_frag(r[0], r[1], rf[0]);
+        split_frag(r[2], r[3], rf[1]);
+        floatx4 G[NQ];
+        float edge_prev[3], edge_next[4];
+        {
+            floatx4 G15 = lay_gemm2<K, LAY>(S, NQ - 1, rf, lane, AL);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) G[q] = lay_gemm2<K, LAY>(S, q, rf, lane, AL);
+            gradient(G15, X[NQ - 1]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gradient(G[q], X[q]);
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+                const float v = __shfl(G15[e + 1], src_prev, 64);
+                edge_prev[e] = (g == 0) ? G[0][3 - e] : v;      // reflect: atoms -3,-2,-1 -> 3,2,1
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) edge_next[e] = __shfl(G[0][e], src_next, 64);
+        }
+        Frag3 F[2][2];
+        ln_load_unit<K, LAY>(S, ln_unit(0, 0, 0), lane, AL, F[0][0]);
+        ln_load_unit<K, LAY>(S, ln_unit(0, 0, 1), lane, AL, F[0][1]);
+        __builtin_amdgcn_sched_barrier(0);
+
+        int carry[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int pp = 0; pp < NQ / 2; ++pp) {
+            const int qa = 2 * pp, qb = qa + 1;
+            // tiles whose products were issued in the previous step get their gradient step
+            if (pp >= 1 && pp <= 6) {
+                gradient(G[qa + 2], X[qa + 2]);
+                gradient(G[qb + 2], X[qb + 2]);
+            }
+            bf16x8 xf[3];
+            if (pp >= 1) split_frag(X[qa - 2], X[qb - 2], xf);
+            double w[11];
+            int W1[7], W2[7], W3[7];
+            float out[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int s = 4 * pp + k, cur = s & 1, nxt = cur ^ 1;
+                // MFMAs of this slot's units
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const LnUnit U = ln_unit(pp, k, u);
+                    if (U.kind == 1) G[U.a] = mfma_split6(F[cur][u].a, rf[U.b], U.b == 0 ? floatx4{0.f, 0.f, 0.f, 0.f} : G[U.a]);
+                    else if (U.kind == 2) R[U.a] = mfma_split6(F[cur][u].a, xf, R[U.a]);
+                }
+                // operands of the next slot
+                const int pn = (k == 3) ? pp + 1 : pp, kn = (k + 1) & 3;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) ln_load_unit<K, LAY>(S, ln_unit(pn, kn, u), lane, AL, F[nxt][u]);
+                // NLM phase
+                const int q = (k < 2) ? qa : qb;
+                if (k == 0 || k == 2) {
+                    float prv[3], nx[4];
+                    if (q == 0) {
+#pragma unroll
+                        for (int e = 0; e < 3; ++e) prv[e] = edge_prev[e];
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 3; ++e) prv[e] = G[q - 1][e + 1];
+                    }
+                    if (q == NQ - 1) {    // reflect: atoms 256..259 -> 254, 253, 252, 251
+                        const float rfl[4] = {G[q][2], G[q][1], G[q][0], G[q - 1][3]};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) nx[e] = (g == 3) ? rfl[e] : edge_next[e];
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) nx[e] = G[q + 1][e];
+                    }
+                    const double wv[11] = {prv[0], prv[1], prv[2], G[q][0], G[q][1], G[q][2], G[q][3],
+                                           nx[0], nx[1], nx[2], nx[3]};
+#pragma unroll
+                    for (int e = 0; e < 11; ++e) w[e] = wv[e];
+                    if (q == 0) {
+                        nlm_weights<true>(w, kneg, W1, W2, W3);
+                    } else {
+                        nlm_weights<false>(w, kneg, W1, W2, W3);
+                        W1[2] = carry[0];
+                        W2[1] = carry[1]; W2[2] = carry[2];
+                        W3[0] = carry[3]; W3[1] = carry[4]; W3[2] = carry[5];
+                    }
+                    carry[0] = W1[6];
+                    carry[1] = W2[5]; carry[2] = W2[6];
+                    carry[3] = W3[4]; carry[4] = W3[5]; carry[5] = W3[6];
+                } else {
+                    nlm_outputs(w, W1, W2, W3, c0, p.seven, out);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) X[q][i] = out[i];
+                }
+                if (GB) {
+#pragma unroll
+                    for (int u = 0; u < 6 * ((ln_unit(pp, k, 0).kind ? 1 : 0) + (ln_unit(pp, k, 1).kind ? 1 : 0)); ++u) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        {
+            bf16x8 xf[3];
+            split_frag(X[NQ - 2], X[NQ - 1], xf);
+            lay_gemm1<K, LAY>(S, NQ / 2 - 1, xf, R, lane, AL);
+        }
+    }
+
+    if (valid) {
+        if (p.coefs) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                *reinterpret_cast<float4 *>(&p.coefs[j * K + 64 * g + 4 * q]) =
                     make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
         }
 #pragma unroll
@@ -962,7 +1584,7 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     if (n_pad <= kStageRows && split && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_b3<256, true>), grid_b3, dim3(kB3Threads), 0, st, p);
     else if (n_pad <= kStageRows && split)
-        hipLaunchKernelGGL((k_ista_b3<256, false>), grid_b3, dim3(kB3Threads), 0, st, p);
+        hipLaunchKernelGGL((k_ista_ln2<256, false, 1>), grid_b3, dim3(kB3Threads), 0, st, p);
     else if (n_pad <= kStageRows && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_res<256, true>), grid, dim3(kIstaThreads), 0, st, p);
     else if (n_pad <= kStageRows)
@@ -982,6 +1604,35 @@ extern "C" int lrs_nlm_col_f32(const float *g, int64_t ldg, float *out, int64_t 
     if (nvec == 0) return LRS_OK;
     hipLaunchKernelGGL(k_nlm_col, dim3((unsigned)nvec), dim3(256), (size_t)(K + 10) * sizeof(float),
                        (hipStream_t)stream, g, ldg, out, ldo, (int)K, h, h_per_vec);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+// Diagnostic entry (not in include/lrspnp.h): variants of the split-bf16 kernel (timing only:
+// 1 no shuffles, 2 no NLM, 3 no MFMA products, 4 two waves per SIMD, 5 sequential tile pair NLM).
+extern "C" int lrs_diag_ista_b3_variant(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,
+                                        int64_t nb, const float *alpha, const double *thr, int Nit, int variant,
+                                        float *phi, void *stream) {
+    if (n_pad > kStageRows || !phi) return LRS_E_INVALID;
+    IstaParams p{Yb, obs, D, alpha, thr, nullptr, phi, (int)n, (int)n_pad, Nit, LRS_PROX_NLM, nb, 7.0};
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g4((unsigned)((nb + 63) / 64)), g8((unsigned)((nb + 127) / 128));
+    switch (variant) {
+    case 0: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 0>), g4, dim3(256), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 1>), g4, dim3(256), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 2>), g4, dim3(256), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 3>), g4, dim3(256), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((k_ista_b3<256, false, 8, false, 0>), g8, dim3(512), 0, st, p); break;
+    case 5: hipLaunchKernelGGL((k_ista_b3<256, false, 4, true, 0>), g4, dim3(256), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 0, 1>), g4, dim3(256), 0, st, p); break;
+    case 7: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 0, 2>), g4, dim3(256), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((k_ista_ln<256, false>), g4, dim3(256), 0, st, p); break;
+    case 9: hipLaunchKernelGGL((k_ista_ln<256, false, 1>), g4, dim3(256), 0, st, p); break;
+    case 10: hipLaunchKernelGGL((k_ista_ln2<256, false>), g4, dim3(256), 0, st, p); break;
+    case 11: hipLaunchKernelGGL((k_ista_ln2<256, true>), g4, dim3(256), 0, st, p); break;
+    case 12: hipLaunchKernelGGL((k_ista_ln2<256, false, 1>), g4, dim3(256), 0, st, p); break;
+    default: return LRS_E_INVALID;
+    }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
