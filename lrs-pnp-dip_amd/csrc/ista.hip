@@ -531,6 +531,15 @@ struct Reuse6 {
     int v[6];   // W1[6], W2[5], W2[6], W3[4], W3[5], W3[6] of a chunk
 };
 
+template <int DIV>
+__device__ __forceinline__ float nlm_div_v(double num, double den) {
+    double r = __builtin_amdgcn_rcp(den);
+    if (DIV == 0) return (float)(num * r);
+    const double e = __fma_rn(-den, r, 1.0);
+    r = __fma_rn(r, e, r);
+    return (float)(num * r);
+}
+
 __device__ __forceinline__ float nlm_div_fast(double num, double den) {
     double r = __builtin_amdgcn_rcp(den);
     const double e = __fma_rn(-den, r, 1.0);
@@ -576,6 +585,7 @@ __device__ __forceinline__ void nlm_weights(const double (&w)[11], double kneg, 
     }
 }
 
+template <int DIV = 2>
 __device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W1)[7], const int (&W2)[7],
                                             const int (&W3)[7], double c0, double seven, float (&out)[4]) {
 #pragma unroll
@@ -590,7 +600,7 @@ __device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W
         const double sw = ((ws[0] + ws[5]) + (ws[1] + ws[4])) + (ws[2] + ws[3]);   // exact
         const double num = __fma_rn(seven, swv, c0 * w[C]);
         const double den = __fma_rn(seven, sw, c0);
-        out[e] = nlm_div_fast(num, den);
+        out[e] = DIV == 2 ? nlm_div_fast(num, den) : nlm_div_v<DIV>(num, den);
     }
 }
 
@@ -1210,7 +1220,7 @@ __device__ __forceinline__ void lay_gemm1(const IstaSmemB3<K> &S, int p, const b
     }
 }
 
-template <int K, bool GB, int LAY = 0>
+template <int K, bool GB, int LAY = 0, bool FOLD = false, int DIV = 2>
 __global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln2(IstaParams p) {
     static_assert(K == 256, "the lane layout assumes 4 groups of 64 atoms");
     constexpr int NQ = K / 16;
@@ -1257,7 +1267,7 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln2(IstaParams p) {
     const float ainv = 1.0f / alpha;
     auto gradient = [&](floatx4 &Gq, const float (&xq)[4]) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Gq[i] = xq[i] + div_by(Gq[i], alpha, ainv);
+        for (int i = 0; i < 4; ++i) Gq[i] = FOLD ? xq[i] + Gq[i] : xq[i] + div_by(Gq[i], alpha, ainv);
     };
 
     for (int it = 0; it < p.Nit; ++it) {
@@ -1265,7 +1275,10 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln2(IstaParams p) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) r[t][i] = ((mres >> (4 * t + i)) & 1u) ? (y[t][i] - R[t][i]) : 0.0f;
+            for (int i = 0; i < 4; ++i) {
+                r[t][i] = ((mres >> (4 * t + i)) & 1u) ? (y[t][i] - R[t][i]) : 0.0f;
+                if (FOLD) r[t][i] = div_by(r[t][i], alpha, ainv);   // D^T (r / alpha)
+            }
             R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
         bf16x8 rf[2][3];
@@ -1356,7 +1369,7 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln2(IstaParams p) {
                     carry[1] = W2[5]; carry[2] = W2[6];
                     carry[3] = W3[4]; carry[4] = W3[5]; carry[5] = W3[6];
                 } else {
-                    nlm_outputs(w, W1, W2, W3, c0, p.seven, out);
+                    nlm_outputs<DIV>(w, W1, W2, W3, c0, p.seven, out);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) X[q][i] = out[i];
                 }
@@ -1584,7 +1597,7 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     if (n_pad <= kStageRows && split && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_b3<256, true>), grid_b3, dim3(kB3Threads), 0, st, p);
     else if (n_pad <= kStageRows && split)
-        hipLaunchKernelGGL((k_ista_ln2<256, false, 1>), grid_b3, dim3(kB3Threads), 0, st, p);
+        hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, 1>), grid_b3, dim3(kB3Threads), 0, st, p);
     else if (n_pad <= kStageRows && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_res<256, true>), grid, dim3(kIstaThreads), 0, st, p);
     else if (n_pad <= kStageRows)
@@ -1631,6 +1644,9 @@ extern "C" int lrs_diag_ista_b3_variant(const float *Yb, const uint8_t *obs, con
     case 10: hipLaunchKernelGGL((k_ista_ln2<256, false>), g4, dim3(256), 0, st, p); break;
     case 11: hipLaunchKernelGGL((k_ista_ln2<256, true>), g4, dim3(256), 0, st, p); break;
     case 12: hipLaunchKernelGGL((k_ista_ln2<256, false, 1>), g4, dim3(256), 0, st, p); break;
+    case 13: hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true>), g4, dim3(256), 0, st, p); break;
+    case 14: hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, 1>), g4, dim3(256), 0, st, p); break;
+    case 15: hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, 0>), g4, dim3(256), 0, st, p); break;
     default: return LRS_E_INVALID;
     }
     LRS_CHECK_LAUNCH();

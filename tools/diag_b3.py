@@ -12,7 +12,7 @@ import torch  # noqa: E402
 from lrspnp import _lib  # noqa: E402
 from lrspnp.data import synthetic_dictionary  # noqa: E402
 
-NAMES = {0: "baseline", 1: "no shuffles", 2: "no NLM", 3: "no MFMA", 4: "2 waves/SIMD", 5: "seq pair NLM", 9: "v9", 10: "ln2", 11: "ln2+gb", 12: "ln2 tile-major",
+NAMES = {0: "baseline", 1: "no shuffles", 2: "no NLM", 3: "no MFMA", 4: "2 waves/SIMD", 5: "seq pair NLM", 9: "v9", 10: "ln2", 11: "ln2+gb", 12: "ln2 tile-major", 13: "+fold alpha", 14: "+fold+div1", 15: "+fold+div0",
          6: "variant6", 7: "variant7", 8: "variant8"}
 L = _lib.device_lib()
 f = L.lrs_diag_ista_b3_variant
@@ -42,10 +42,10 @@ for rep in range(4):
         torch.cuda.synchronize()
         if rep:
             times[v].append(e0.elapsed_time(e1))
-        if rep == 0 and v == 0:
+        if rep == 0 and v == variants[0]:
             ref = phi.clone()
-        if rep == 0 and v != 0:
+        elif rep == 0:
             d = float((phi - ref).norm() / ref.norm())
-            print(f"variant {v}: rel diff vs baseline {d:.3e}", flush=True)
+            print(f"variant {v}: rel diff vs variant {variants[0]} {d:.3e}", flush=True)
 for v in variants:
     print(f"{v} {NAMES[v]:>16s}: {np.median(times[v]):8.3f} ms", flush=True)
