@@ -103,15 +103,23 @@ int lrs_ista_get_precision(void);
 
 /* ---- SVT low-rank prox ---------------------------------------------------------------------
  * U = SVT(Z, tau) with Z = X + c2 * L2 (c2 = float(1/mu_2); L2 may be NULL), via an fp64 Gram
- * Z^T Z, a one-workgroup Jacobi eigensolver (warm-started from the previous call's eigenvectors
- * kept in ws when warm != 0) and U = Z * V diag(max(1 - tau/s, 0)) V^T.  s_out (nullable,
- * device, B doubles) receives the singular values (descending). */
+ * Z^T Z, a one-workgroup symmetric eigensolver and U = Z * V diag(max(1 - tau/s, 0)) V^T.
+ * `warm` is a flag word:
+ *   default (0): Householder tridiagonalisation + multisection + inverse iteration with a
+ *     Davis-Kahan orthogonality certificate, falling back (inside the same workgroup) to the
+ *     Jacobi solve when the certificate fails (clustered / repeated eigenvalues);
+ *   LRS_SVT_JACOBI: the cyclic Jacobi solver only, warm-started from the previous call's
+ *     eigenvectors kept in ws when LRS_SVT_WARM is also set.
+ * s_out (nullable, device, B doubles) receives the singular values (descending). */
+#define LRS_SVT_WARM 1
+#define LRS_SVT_JACOBI 2
 size_t lrs_svt_workspace(int64_t P, int64_t B);
 int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau,
                 float *U, double *s_out, int warm, void *ws, size_t ws_bytes, void *stream);
 /* The same call split in two stream-ordered halves so the caller can start the sparse-coding
- * kernel between them: _gram (multi-workgroup Gram + warm-start products, ~0.3 ms) and _finish
- * (one-workgroup eigensolver + V update + U, which then runs beside the sparse coding). */
+ * kernel between them: _gram (multi-workgroup Gram, plus the warm-start products for
+ * LRS_SVT_JACOBI | LRS_SVT_WARM) and _finish (the one-workgroup eigensolver, then U), which then
+ * runs beside the sparse coding. */
 int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, int warm,
                      void *ws, size_t ws_bytes, void *stream);
 int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau,

@@ -15,6 +15,8 @@
 // The whole chain runs on its own stream beside the sparse-coding kernel.
 #include <math.h>
 
+#include <algorithm>
+
 #include "lrs_common.h"
 
 namespace lrs {
@@ -34,8 +36,11 @@ struct SvtWs {
     double *V[2];     // [Bp][Bp]  eigenvectors, double-buffered
     double *lam;      // [Bp]      eigenvalues (diag of the converged A)
     double *rot;      // [kMaxSweeps*(Bp-1)][Bp/2][2]  (c, s) per round and pair
+    double *beta;     // [Bp]      Householder scalars (tridiagonal path)
+    double *F;        // [Bp][4][Bp] pivoted LU rows of T - lambda_i I (inverse iteration)
     float *E;         // [B][B]
-    int *state;       // [0] V valid, [1] current V buffer, [2] rounds, [3] sweeps
+    int *state;       // [0] V valid, [1] current V buffer, [2] rounds, [3] sweeps,
+                      // [4] path of the last solve (1 tridiagonal, 2 Jacobi fallback, 3 Jacobi)
     int64_t nslab, ntp, Bp;
 };
 
@@ -63,6 +68,8 @@ static SvtWs svt_ws_layout(void *base, int64_t P, int64_t B) {
     w.V[1] = (double *)take(mat);
     w.lam = (double *)take((size_t)w.Bp * sizeof(double));
     w.rot = (double *)take((size_t)kMaxSweeps * (w.Bp - 1) * (w.Bp / 2) * 2 * sizeof(double));
+    w.beta = (double *)take((size_t)w.Bp * sizeof(double));
+    w.F = (double *)take((size_t)4 * mat);
     w.E = (float *)take((size_t)B * B * sizeof(float));
     return w;
 }
@@ -199,8 +206,8 @@ __device__ __forceinline__ double wg_reduce(double v, double *red) {
     return s;
 }
 
-__global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm) {
-    extern __shared__ double sm[];
+// The solve on A = src (packed into LDS), eigenvalues to w.lam, rounds/sweeps to w.state[2..3].
+__device__ __noinline__ void jacobi_core(double *sm, SvtWs w, const double *src) {
     const int Bp = (int)w.Bp, half = Bp / 2;
     const int npk = Bp * (Bp + 1) / 2;
     double *A = sm;                      // packed upper triangle
@@ -209,8 +216,6 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
     __shared__ int any_rot;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
-    const bool use_warm = warm && w.state[0] == 1;
-    const double *src = use_warm ? w.A0 : w.G;
     for (int i = tid; i < Bp; i += kJacobiThreads) rowoff[i] = i * Bp - (i * (i - 1)) / 2 - i;
     __syncthreads();
     for (int i = 0; i < Bp; ++i)
@@ -292,6 +297,13 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
         w.state[2] = rounds;
         w.state[3] = sweeps;
     }
+    __syncthreads();   // rotation log and eigenvalues visible to the workgroup (in-kernel fallback)
+}
+
+__global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm) {
+    extern __shared__ double sm[];
+    const bool use_warm = warm && w.state[0] == 1;
+    jacobi_core(sm, w, use_warm ? w.A0 : w.G);
 }
 
 // ---- 4. V_new = V_old J_1 ... J_R, 64 rows per 1024-thread workgroup, rows in LDS ------------
@@ -300,21 +312,16 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
 constexpr int kVRows = 64;
 constexpr int kLogRounds = 16;
 
-__global__ __launch_bounds__(1024) void k_jacobi_vrebuild(SvtWs w, int warm) {
-    extern __shared__ double vsm[];
+// Rows i0 .. i0+63 of Vn = Vo J_1 ... J_R (Vo = identity when null); 1024 threads.
+__device__ __noinline__ void vrebuild_tile(double *vsm, SvtWs w, const double *Vo, double *Vn, int i0) {
     const int Bp = (int)w.Bp, half = Bp / 2;
     double *vrow = vsm;                                   // [kVRows][Bp]
     double *lcs = vrow + kVRows * Bp;                     // [kLogRounds][half][2]
     short *lpq = (short *)(lcs + kLogRounds * half * 2);  // [kLogRounds][half][2]
-    const int i0 = blockIdx.x * kVRows;
     const int nrows = min(kVRows, Bp - i0);
-    const bool use_warm = warm && w.state[0] == 1;
-    const int cur = w.state[1];
-    const double *Vo = w.V[cur];
-    double *Vn = w.V[cur ^ 1];
     for (int idx = threadIdx.x; idx < nrows * Bp; idx += 1024) {
         const int rr = idx / Bp, j = idx % Bp, i = i0 + rr;
-        vrow[rr * Bp + j] = use_warm ? Vo[(int64_t)i * Bp + j] : (i == j ? 1.0 : 0.0);
+        vrow[rr * Bp + j] = Vo ? Vo[(int64_t)i * Bp + j] : (i == j ? 1.0 : 0.0);
     }
     const int rounds = w.state[2];
     const int rr = threadIdx.x >> 4, kk = threadIdx.x & 15;
@@ -356,10 +363,130 @@ __global__ __launch_bounds__(1024) void k_jacobi_vrebuild(SvtWs w, int warm) {
     }
 }
 
+__global__ __launch_bounds__(1024) void k_jacobi_vrebuild(SvtWs w, int warm) {
+    extern __shared__ double vsm[];
+    const bool use_warm = warm && w.state[0] == 1;
+    const int cur = w.state[1];
+    vrebuild_tile(vsm, w, use_warm ? w.V[cur] : nullptr, w.V[cur ^ 1], blockIdx.x * kVRows);
+}
+
 __global__ void k_svt_finish_state(SvtWs w) {
     // flip the current-V buffer; V is now valid for warm starts
     w.state[1] ^= 1;
     w.state[0] = 1;
+    w.state[4] = 3;
+}
+
+}  // namespace lrs
+
+#include <float.h>
+
+#include "svt_eig.h"
+
+namespace lrs {
+
+// ---- 3'. the whole eigen chain in one workgroup: tridiagonal path, Jacobi fallback, E ---------
+// V -> w.V[state[1]], eigenvalues -> w.lam, E -> w.E; state[0] = 1 (V valid), state[4] = path.
+// Certificate of the tridiagonal path (else the Jacobi fallback on the same G):
+//   * max |V^T V - I| <= kEigOrth0 before, and <= kEigOrth after <= 3 Newton-Schulz steps;
+//   * per vector, ||T w_i - lambda_i w_i|| plus the mixing the orthogonalisation adds,
+//     0.5 ||((lambda_j - lambda_i) (S - I)_ji)_j||, at most kEigRes * ||T||.
+// E = f(G) then differs from the exact matrix function by O(kEigRes ||T|| max|f'|).
+constexpr double kEigOrth0 = 0.05, kEigOrth = 1e-13, kEigRes = 1e-11;
+__global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double tau) {
+    extern __shared__ double sm[];
+    __shared__ double shb[2], red[kEigThreads / 64];
+    const int n = (int)w.Bp, tid = threadIdx.x;
+    unsigned long long *ts = (unsigned long long *)(w.state + 16);   // phase timestamps (100 MHz)
+    if (tid == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
+    double *A = sm;
+    double *pv = A + (size_t)n * (n + 1) / 2;      // [n] p vector, then the eigenvalues
+    for (int e0 = tid; e0 < n * n; e0 += 8 * kEigThreads) {
+        double g[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + u * kEigThreads;
+            g[u] = e < n * n ? w.G[e] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + u * kEigThreads, i = e / n, j = e - i * n;
+            if (e < n * n && j >= i) A[pk_idx(i, j, n)] = g[u];
+        }
+    }
+    __syncthreads();
+    eig_tridiag(A, pv, shb, n, w.beta);
+    if (tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
+    // Gershgorin interval and the tridiagonal's scale (every thread, broadcast reads)
+    double gl = 1e300, gu = -1e300, emax2 = 0.0;
+    {
+        int idx = 0;
+        double ep = 0.0;
+        for (int j = 0; j < n; ++j) {
+            const double e = (j + 1 < n) ? fabs(A[idx + 1]) : 0.0;
+            gl = fmin(gl, A[idx] - ep - e);
+            gu = fmax(gu, A[idx] + ep + e);
+            emax2 = fmax(emax2, e * e);
+            ep = e;
+            if (j + 1 < n) idx += n - j;
+        }
+    }
+    const double tn = fmax(fmax(fabs(gl), fabs(gu)), 1e-300);
+    gl -= 4.0 * DBL_EPSILON * tn * n;
+    gu += 4.0 * DBL_EPSILON * tn * n;
+    const double pivmin = 1e-290 * fmax(1.0, emax2);
+    eig_values(A, n, gl, gu, tn, pivmin, pv, w.lam);
+    __syncthreads();
+    if (tid == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
+    const double res = eig_vectors(A, pv, n, tn, w.F, w.T);
+    __syncthreads();
+    if (tid == 0) ts[3] = __builtin_amdgcn_s_memrealtime();
+    for (int k = tid; k < n - 2; k += kEigThreads) pv[k] = w.beta[k];   // the eigenvalues are in w.lam
+    __syncthreads();
+    eig_backtransform(A, pv, n, w.T, w.V[0]);
+    __syncthreads();
+    if (tid == 0) ts[4] = __builtin_amdgcn_s_memrealtime();
+    // certificate + orthogonalisation (LDS of the reflectors is free from here on)
+    int cur = 0;
+    double dev = eig_syrk<true, 1>(sm, w.V[0], n, nullptr, 0.0, 0, nullptr, w.A0, red);
+    bool bad = !(dev <= kEigOrth0);
+    if (!bad) {
+        double mix = 0.0;
+        if (tid < n) {
+            const double li = w.lam[tid];
+            for (int j = 0; j < n; ++j) {
+                const double m = (w.lam[j] - li) * (w.A0[(int64_t)j * n + tid] - (j == tid ? 1.0 : 0.0));
+                mix = __fma_rn(m, m, mix);
+            }
+        }
+        const double bound = res + 0.5 * sqrt(mix);
+        bad = __syncthreads_or(!(bound <= kEigRes * tn));
+    }
+    for (int step = 0; step < 3 && !bad && dev > kEigOrth; ++step) {
+        eig_ns_step(sm, w.V[cur], w.A0, n, w.V[cur ^ 1]);
+        cur ^= 1;
+        dev = eig_syrk<true, 1>(sm, w.V[cur], n, nullptr, 0.0, 0, nullptr, w.A0, red);
+    }
+    bad = bad || !(dev <= kEigOrth);
+    if (tid == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
+    if (bad) {
+        // clustered / repeated eigenvalues: the orthogonal Jacobi basis of the same G
+        __syncthreads();
+        jacobi_core(sm, w, w.G);
+        cur = 0;
+        for (int i0 = 0; i0 < n; i0 += kVRows) {
+            vrebuild_tile(sm, w, nullptr, w.V[0], i0);
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {
+        w.state[0] = 1;
+        w.state[1] = cur;
+        w.state[4] = bad ? 2 : 1;
+    }
+    __syncthreads();
+    eig_syrk<false, 0>(sm, w.V[cur], n, w.lam, tau, B, w.E, nullptr, red);
+    if (tid == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---- 5a. E = V diag(e) V^T, e_k = min(tau/s_k, 1); s_out = sorted singular values -----------
@@ -588,7 +715,7 @@ extern "C" int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64
     hipLaunchKernelGGL(k_gram_reduce, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 4096)), dim3(256), 0, st,
                        w.partial, w.nslab, (int)w.ntp, nt, (int)B, Bp, w.G);
     LRS_CHECK_LAUNCH();
-    if (warm) {
+    if ((warm & LRS_SVT_WARM) && (warm & LRS_SVT_JACOBI)) {
         // A0 = V^T (G V) with the current V (unused when V is not valid yet: Jacobi starts from G)
         const dim3 g16((Bp + 15) / 16, (Bp + 15) / 16);
         hipLaunchKernelGGL(k_gemm_f64_state, g16, dim3(256), 0, st, w, 0);
@@ -611,22 +738,35 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
     const size_t smem = sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp + 16) + sizeof(int) * (2 * Bp);
     const size_t vsmem = sizeof(double) * ((size_t)kVRows * Bp + (size_t)kLogRounds * (Bp / 2) * 2) +
                          sizeof(short) * (size_t)kLogRounds * (Bp / 2) * 2;
-    // dynamic LDS above 64 KiB must be opted into; request exactly what this shape needs
-    hipError_t ea = hipFuncSetAttribute((const void *)k_jacobi_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)smem);
-    if (ea != hipSuccess) return (int)ea;
-    ea = hipFuncSetAttribute((const void *)k_jacobi_vrebuild, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vsmem);
-    if (ea != hipSuccess) return (int)ea;
-    hipLaunchKernelGGL(k_jacobi_lds, dim3(1), dim3(kJacobiThreads), smem, st, w, warm);
-    LRS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_jacobi_vrebuild, dim3((unsigned)((Bp + kVRows - 1) / kVRows)), dim3(1024), vsmem, st, w,
-                       warm);
-    LRS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_svt_finish_state, dim3(1), dim3(1), 0, st, w);
-    LRS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_build_E, dim3((unsigned)((B + 15) / 16), (unsigned)((B + 15) / 16)), dim3(256), 0, st, w,
-                       (int)B, tau);
-    LRS_CHECK_LAUNCH();
+    if (warm & LRS_SVT_JACOBI) {
+        const int jwarm = warm & LRS_SVT_WARM;
+        // dynamic LDS above 64 KiB must be opted into; request exactly what this shape needs
+        hipError_t ea = hipFuncSetAttribute((const void *)k_jacobi_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)smem);
+        if (ea != hipSuccess) return (int)ea;
+        ea = hipFuncSetAttribute((const void *)k_jacobi_vrebuild, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)vsmem);
+        if (ea != hipSuccess) return (int)ea;
+        hipLaunchKernelGGL(k_jacobi_lds, dim3(1), dim3(kJacobiThreads), smem, st, w, jwarm);
+        LRS_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_jacobi_vrebuild, dim3((unsigned)((Bp + kVRows - 1) / kVRows)), dim3(1024), vsmem, st,
+                           w, jwarm);
+        LRS_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_svt_finish_state, dim3(1), dim3(1), 0, st, w);
+        LRS_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_build_E, dim3((unsigned)((B + 15) / 16), (unsigned)((B + 15) / 16)), dim3(256), 0, st,
+                           w, (int)B, tau);
+        LRS_CHECK_LAUNCH();
+    } else {
+        const size_t tsmem = sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp);
+        const size_t esmem = sizeof(double) * 2 * kEKc * kELd;
+        const size_t lds = std::max(std::max(tsmem, esmem), std::max(smem, vsmem));
+        hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)lds);
+        if (ea != hipSuccess) return (int)ea;
+        hipLaunchKernelGGL(k_svt_eig, dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau);
+        LRS_CHECK_LAUNCH();
+    }
     if (s_out) {
         hipLaunchKernelGGL(k_sorted_singular_values, dim3(1), dim3(256), 0, st, w, (int)B, s_out);
         LRS_CHECK_LAUNCH();
@@ -656,8 +796,10 @@ extern "C" int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P,
     return lrs_svt_finish_f32(X, L2, c2, P, B, tau, U, s_out, warm, ws, ws_bytes, stream);
 }
 
-// Diagnostics (not in include/lrspnp.h): Jacobi rounds / sweeps of the last call (host copy).
-extern "C" int lrs_diag_svt_state(void *ws, int64_t P, int64_t B, int *out4) {
+// Diagnostics (not in include/lrspnp.h): state words of the last call (host copy): V valid, V buffer,
+// Jacobi rounds, sweeps, path (1 tridiagonal, 2 Jacobi fallback, 3 Jacobi), 11 spare, then 8 u64
+// phase timestamps of the tridiagonal path (s_memrealtime, 100 MHz).
+extern "C" int lrs_diag_svt_state(void *ws, int64_t P, int64_t B, int *out32) {
     SvtWs w = svt_ws_layout(ws, P, B);
-    return (int)hipMemcpy(out4, w.state, 4 * sizeof(int), hipMemcpyDeviceToHost);
+    return (int)hipMemcpy(out32, w.state, 32 * sizeof(int), hipMemcpyDeviceToHost);
 }

@@ -141,8 +141,18 @@ def svt_workspace(P: int, B: int, device) -> torch.Tensor:
     return torch.zeros(n, dtype=torch.uint8, device=device)
 
 
-def svt(X, L2, c2: float, tau: float, ws, U=None, s_out=None, warm=False, stream=None):
-    """U = SVT(X + c2*L2, tau) (main_LRS_PnP.py:118-124)."""
+SVT_WARM, SVT_JACOBI = 1, 2          # include/lrspnp.h flag word of the svt calls
+
+
+def _svt_flags(warm, method):
+    if method not in ("tri", "jacobi"):
+        raise LrsError(f"unknown SVT eigensolver {method!r} (tri | jacobi)")
+    return (SVT_WARM if warm else 0) | (SVT_JACOBI if method == "jacobi" else 0)
+
+
+def svt(X, L2, c2: float, tau: float, ws, U=None, s_out=None, warm=False, stream=None, method="tri"):
+    """U = SVT(X + c2*L2, tau) (main_LRS_PnP.py:118-124).  method 'tri': tridiagonal eigensolver
+    with a certified Jacobi fallback (default); 'jacobi': Jacobi only (warm-startable)."""
     L = device_lib()
     _dev(X, torch.float32, "X")
     if L2 is not None:
@@ -150,33 +160,42 @@ def svt(X, L2, c2: float, tau: float, ws, U=None, s_out=None, warm=False, stream
     P, B = X.shape
     if U is None:
         U = torch.empty_like(X)
-    check(L.lrs_svt_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out), int(bool(warm)), _p(ws),
-                        ws.numel(), _s(stream)), "lrs_svt_f32")
+    check(L.lrs_svt_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out), _svt_flags(warm, method),
+                        _p(ws), ws.numel(), _s(stream)), "lrs_svt_f32")
     return U
 
 
-def svt_gram(X, L2, c2: float, ws, warm=False, stream=None):
-    """First half of svt(): fp64 Gram (+ warm-start product), multi-workgroup."""
+def svt_gram(X, L2, c2: float, ws, warm=False, stream=None, method="tri"):
+    """First half of svt(): fp64 Gram (+ the Jacobi warm-start product), multi-workgroup."""
     L = device_lib()
     P, B = X.shape
-    check(L.lrs_svt_gram_f32(_p(X), _p(L2), float(c2), P, B, int(bool(warm)), _p(ws), ws.numel(), _s(stream)),
-          "lrs_svt_gram_f32")
+    check(L.lrs_svt_gram_f32(_p(X), _p(L2), float(c2), P, B, _svt_flags(warm, method), _p(ws), ws.numel(),
+                             _s(stream)), "lrs_svt_gram_f32")
 
 
-def svt_finish(X, L2, c2: float, tau: float, ws, U, s_out=None, warm=False, stream=None):
-    """Second half of svt(): one-workgroup Jacobi, V update, U = Z - Z E."""
+def svt_finish(X, L2, c2: float, tau: float, ws, U, s_out=None, warm=False, stream=None, method="tri"):
+    """Second half of svt(): the one-workgroup eigensolver, E, then U = Z - Z E."""
     L = device_lib()
     P, B = X.shape
-    check(L.lrs_svt_finish_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out), int(bool(warm)),
-                               _p(ws), ws.numel(), _s(stream)), "lrs_svt_finish_f32")
+    check(L.lrs_svt_finish_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out),
+                               _svt_flags(warm, method), _p(ws), ws.numel(), _s(stream)), "lrs_svt_finish_f32")
     return U
 
 
 def svt_state(ws, P: int, B: int):
-    """(V valid, V buffer, Jacobi rounds, sweeps) of the last SVT call (diagnostics; syncs)."""
-    out = (ctypes.c_int * 4)()
+    """(V valid, V buffer, Jacobi rounds, sweeps, path, -, -, -) of the last SVT call, path 1 =
+    tridiagonal, 2 = Jacobi fallback, 3 = Jacobi (diagnostics; syncs)."""
+    out = (ctypes.c_int * 32)()
     check(device_lib().lrs_diag_svt_state(_p(ws), P, B, ctypes.cast(out, ctypes.c_void_p)), "lrs_diag_svt_state")
     return list(out)
+
+
+def svt_phase_us(ws, P: int, B: int):
+    """Phase durations (us) of the last tridiagonal-path solve: load+tridiagonalise, eigenvalues,
+    inverse iteration, back-transformation, certificate/orthogonalisation, fallback+E (syncs)."""
+    st = np.array(svt_state(ws, P, B), dtype=np.int32)
+    t = st[16:32].view(np.uint64).astype(np.float64)
+    return [(t[k + 1] - t[k]) / 100.0 for k in range(6)]
 
 
 def admm_update(X, L1, L2, Y, M, U, phi, bb, grid, gamma, mu1, mu2, norms=None, imout=None, stream=None):

@@ -31,7 +31,9 @@ class LrsPnPConfig:
     bb: int = 36                  # block size                          :237
     sliding: int = 36             # slidingDis                          :238
     variant: str = "spec2"        # 'spec2' (main), 'fro4' (DIP mains), 'soft' (ista.m)
+    svt_method: str = "tri"       # SVT eigensolver: 'tri' (tridiagonal, certified) or 'jacobi'
     svt_warm: bool = True         # warm-start the Jacobi eigensolver from the previous iteration
+    svt_gram_first: bool = False  # hold the sparse coding until the SVT Gram is done (always for Jacobi)
     lowrank: str = "svt"          # 'svt' (main_LRS_PnP.py:315) or 'dip' (…1-LiP.py:399-411)
     dip: object = None            # lrspnp.dip.DipConfig for lowrank='dip' (None: reference defaults)
     dip_seed: int = 0             # DIP init seed of outer iteration t is dip_seed + t
@@ -162,7 +164,7 @@ class LrsPnP:
     def low_rank(self, stream=None, s_out=None):
         warm = self.cfg.svt_warm and self.iteration > 0
         return ops.svt(self.X, self.L2, self.c2, self.tau, self.svt_ws, U=self.U, s_out=s_out, warm=warm,
-                       stream=stream)
+                       stream=stream, method=self.cfg.svt_method)
 
     def low_rank_dip(self, stream):
         """U = DIP(X + L2/mu2) (…1-LiP.py:399-411) on `stream`; the host polls early stopping."""
@@ -182,14 +184,19 @@ class LrsPnP:
         lr = self.lowrank_stream
         warm = self.cfg.svt_warm and self.iteration > 0
         lr.wait_stream(main)
-        # low-rank prox, first half (whole chip, ~0.3 ms): fp64 Gram + warm-start products
-        ops.svt_gram(self.X, self.L2, self.c2, self.svt_ws, warm=warm, stream=lr)
+        # low-rank prox, first half (whole chip, ~0.2 ms): fp64 Gram (+ Jacobi warm-start products)
+        ops.svt_gram(self.X, self.L2, self.c2, self.svt_ws, warm=warm, stream=lr, method=self.cfg.svt_method)
         gram_done = lr.record_event()
         # second half: the one-workgroup eigensolver then runs beside the sparse coding
-        ops.svt_finish(self.X, self.L2, self.c2, self.tau, self.svt_ws, self.U, warm=warm, stream=lr)
+        ops.svt_finish(self.X, self.L2, self.c2, self.tau, self.svt_ws, self.U, warm=warm, stream=lr,
+                       method=self.cfg.svt_method)
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
                    stream=main)
-        main.wait_event(gram_done)
+        if self.cfg.svt_gram_first or self.cfg.svt_method == "jacobi":
+            # the Gram gets the chip before the sparse-coding kernel fills it, so the ~7 ms Jacobi
+            # solve starts at once; the tridiagonal chain fits inside the sparse coding even when
+            # its Gram waits for the first sparse-coding workgroups to retire
+            main.wait_event(gram_done)
         ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
                  stream=main)
         main.wait_stream(lr)

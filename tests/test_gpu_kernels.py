@@ -164,8 +164,10 @@ def test_alpha_kernel_vs_numpy(ops, n, variant):
 
 
 # ------------------------------------------------------------------------------------------ SVT
-@pytest.mark.parametrize("P,B,rank,noise", [(1296, 128, 8, 0.12), (4000, 198, 8, 0.02), (500, 60, 3, 0.002)])
-def test_svt_kernel_vs_numpy(ops, P, B, rank, noise):
+@pytest.mark.parametrize("method", ["tri", "jacobi"])
+@pytest.mark.parametrize("P,B,rank,noise", [(1296, 128, 8, 0.12), (4000, 198, 8, 0.02), (500, 60, 3, 0.002),
+                                            (777, 45, 5, 0.05)])
+def test_svt_kernel_vs_numpy(ops, P, B, rank, noise, method):
     rng = np.random.default_rng(P + B)
     Z = (rng.random((P, rank)) @ rng.random((rank, B)) * 0.3 + noise * rng.standard_normal((P, B)))
     X = Z.astype(np.float32)
@@ -176,14 +178,43 @@ def test_svt_kernel_vs_numpy(ops, P, B, rank, noise):
     d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     ws = ops.svt_workspace(P, B, "cuda")
     s = torch.empty(B, dtype=torch.float64, device="cuda")
-    U = ops.svt(d(X), d(L2), c2, tau, ws, s_out=s, warm=False).cpu().numpy()
+    U = ops.svt(d(X), d(L2), c2, tau, ws, s_out=s, warm=False, method=method).cpu().numpy()
     assert rel(U, ref) < 1e-5
     sref = np.linalg.svd((X + c2 * L2).astype(np.float64), compute_uv=False)
     assert rel(s.cpu().numpy(), sref) < 1e-9
+    path = ops.svt_state(ws, P, B)[4]
+    assert path == (1 if method == "tri" else 3), path     # the tridiagonal path certified itself
     # warm start from the previous eigenvectors on a perturbed matrix
     X2 = (X + 1e-3 * rng.standard_normal((P, B))).astype(np.float32)
-    U2 = ops.svt(d(X2), d(L2), c2, tau, ws, warm=True).cpu().numpy()
+    U2 = ops.svt(d(X2), d(L2), c2, tau, ws, warm=True, method=method).cpu().numpy()
     assert rel(U2, O.svt(X2 + c2 * L2, 1 / 0.9)) < 1e-5
+
+
+@pytest.mark.parametrize("B", [64, 197])
+@pytest.mark.parametrize("exact", [True, False])
+def test_svt_repeated_singular_values(ops, B, exact):
+    """Repeated singular values.  exact: Z = 2 [I; 0] plus a rank-3 term on rows the identity does
+    not touch, so the Gram has the eigenvalue 4 exactly B - 3 times and T splits into identical
+    blocks: inverse iteration returns non-orthogonal vectors, the certificate fails and the
+    workgroup falls back to Jacobi.  Otherwise (float32-rounded orthonormal columns, a tight
+    cluster) the Newton-Schulz repair keeps the tridiagonal path.  U matches LAPACK either way."""
+    rng = np.random.default_rng(B)
+    P = 3 * B
+    if exact:
+        X = np.zeros((P, B), np.float32)
+        X[:B, :B] = 2.0 * np.eye(B, dtype=np.float32)
+        X[B:, :3] = (0.5 * rng.standard_normal((P - B, 3))).astype(np.float32)
+    else:
+        Q, _ = np.linalg.qr(rng.standard_normal((P, B)))
+        X = (2.0 * Q).astype(np.float32)
+        X[:, :3] += (0.5 * rng.standard_normal((P, 3))).astype(np.float32)
+    ref = O.svt(X, 1 / 0.9)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    ws = ops.svt_workspace(P, B, "cuda")
+    U = ops.svt(d(X), None, 1.0, float(np.float32(1 / 0.9)), ws).cpu().numpy()
+    assert rel(U, ref) < 1e-5
+    path = ops.svt_state(ws, P, B)[4]
+    assert path == (2 if exact else 1), path
 
 
 # ------------------------------------------------------------------------------------------ ADMM
