@@ -264,7 +264,7 @@ def main():
         "config": {"workload": f"LRS-PnP (no DIP) {args.cube} cube, {args.bb}x{args.bb} blocks, K={K}, "
                                f"Nit={args.nit} inner ISTA, SVT low-rank prox (BASELINE configs[1])",
                    "blocks": nb, "parallelism": f"{world} independent cube(s), one per GPU"},
-        "roofline": {"bound": "mfma", "kernel": "k_ista_b3 (lrs_ista_f32)", "achieved": achieved,
+        "roofline": {"bound": "mfma", "kernel": "k_ista_ln2 (lrs_ista_f32)", "achieved": achieved,
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                      "traffic": traffic, "flops_per_launch": flops, "ms_per_launch": ista_ms},
         "setup_s": setup_s,

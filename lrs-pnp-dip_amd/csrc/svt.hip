@@ -393,7 +393,7 @@ namespace lrs {
 //     0.5 ||((lambda_j - lambda_i) (S - I)_ji)_j||, at most kEigRes * ||T||.
 // E = f(G) then differs from the exact matrix function by O(kEigRes ||T|| max|f'|).
 constexpr double kEigOrth0 = 0.05, kEigOrth = 1e-13, kEigRes = 1e-11;
-__global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double tau) {
+__global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double tau, int dbg) {
     extern __shared__ double sm[];
     __shared__ double shb[2], red[kEigThreads / 64];
     const int n = (int)w.Bp, tid = threadIdx.x;
@@ -417,6 +417,12 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double 
     __syncthreads();
     eig_tridiag(A, pv, shb, n, w.beta);
     if (tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
+    if (dbg)   // diagnostics: the tridiagonal T (d, e) into the Gram partial buffer
+        for (int j = tid; j < n; j += kEigThreads) {
+            const int idx = pk_idx(j, j, n);
+            w.partial[j] = A[idx];
+            w.partial[n + j] = (j + 1 < n) ? A[idx + 1] : 0.0;
+        }
     // Gershgorin interval and the tridiagonal's scale (every thread, broadcast reads)
     double gl = 1e300, gu = -1e300, emax2 = 0.0;
     {
@@ -469,6 +475,10 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double 
     }
     bad = bad || !(dev <= kEigOrth);
     if (tid == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
+    if (dbg) {   // diagnostics: keep the tridiagonal path's V (no fallback, no E)
+        if (tid == 0) { w.state[1] = cur; w.state[4] = bad ? 2 : 1; }
+        return;
+    }
     if (bad) {
         // clustered / repeated eigenvalues: the orthogonal Jacobi basis of the same G
         __syncthreads();
@@ -764,7 +774,7 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
         hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)lds);
         if (ea != hipSuccess) return (int)ea;
-        hipLaunchKernelGGL(k_svt_eig, dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau);
+        hipLaunchKernelGGL(k_svt_eig, dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau, 0);
         LRS_CHECK_LAUNCH();
     }
     if (s_out) {
@@ -802,4 +812,31 @@ extern "C" int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P,
 extern "C" int lrs_diag_svt_state(void *ws, int64_t P, int64_t B, int *out32) {
     SvtWs w = svt_ws_layout(ws, P, B);
     return (int)hipMemcpy(out32, w.state, 32 * sizeof(int), hipMemcpyDeviceToHost);
+}
+
+// Diagnostics: the tridiagonal path on the Gram already in ws (after lrs_svt_gram_f32), no fallback,
+// leaving T (d, e) in the partial buffer, eigenvalues in lam, W in T, V in V[state[1]], S in A0.
+extern "C" int lrs_diag_svt_eig(void *ws, int64_t P, int64_t B, double *out, void *stream) {
+    SvtWs w = svt_ws_layout(ws, P, B);
+    const int Bp = (int)w.Bp;
+    const size_t smem = std::max(sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp + 16) + sizeof(int) * (2 * Bp),
+                                 sizeof(double) * 2 * kEKc * kELd);
+    hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (ea != hipSuccess) return (int)ea;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_svt_eig, dim3(1), dim3(kEigThreads), smem, st, w, (int)B, 1.0, 1);
+    LRS_CHECK_LAUNCH();
+    // out: d[Bp], e[Bp], lam[Bp], W[Bp*Bp], V[Bp*Bp], S[Bp*Bp]
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return (int)e;
+    int state[8];
+    e = hipMemcpy(state, w.state, sizeof(state), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return (int)e;
+    const size_t m = (size_t)Bp * Bp;
+    hipMemcpy(out, w.partial, 2 * Bp * sizeof(double), hipMemcpyDeviceToHost);
+    hipMemcpy(out + 2 * Bp, w.lam, Bp * sizeof(double), hipMemcpyDeviceToHost);
+    hipMemcpy(out + 3 * Bp, w.T, m * sizeof(double), hipMemcpyDeviceToHost);
+    hipMemcpy(out + 3 * Bp + m, w.V[state[1]], m * sizeof(double), hipMemcpyDeviceToHost);
+    e = hipMemcpy(out + 3 * Bp + 2 * m, w.A0, m * sizeof(double), hipMemcpyDeviceToHost);
+    return e != hipSuccess ? (int)e : state[4];
 }

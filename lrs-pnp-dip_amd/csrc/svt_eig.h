@@ -56,11 +56,14 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
     return rl64(v, 63);
 }
 
-// element j (uniform) of a wave-distributed vector r[t] = x[lane + 64 t]
+// element j (uniform) of a wave-distributed vector r[t] = x[lane + 64 t].  readlane reads the
+// source lane's register whatever the EXEC mask, so it must be applied to the registers every lane
+// loaded (r[t]) and the choice among them made afterwards: a vector select in front of it would
+// leave the inactive lanes' values unwritten.
 __device__ __forceinline__ double wdist(const double (&r)[4], int j) {
     const int t = j >> 6, l = j & 63;
-    const double v = t == 0 ? r[0] : t == 1 ? r[1] : t == 2 ? r[2] : r[3];
-    return rl64(v, l);
+    const double v0 = rl64(r[0], l), v1 = rl64(r[1], l), v2 = rl64(r[2], l), v3 = rl64(r[3], l);
+    return t == 0 ? v0 : t == 1 ? v1 : t == 2 ? v2 : v3;
 }
 
 // ---- A. tridiagonalisation: A (packed, LDS) -> T on its diagonal / first superdiagonal --------
@@ -217,6 +220,9 @@ __device__ __noinline__ void eig_values(const double *A, int n, double gl, doubl
         dr[t] = (j < n) ? A[pk_idx(j, j, n)] : 0.0;
         const double e = (j >= 1 && j < n) ? A[pk_idx(j - 1, j - 1, n) + 1] : 0.0;
         er[t] = e * e;
+        // every lane's copy is read by readlane below, including lanes that leave early: keep the
+        // loads ahead of the exit (the compiler may otherwise sink them into the active region)
+        __asm__ volatile("" ::"v"(dr[t]), "v"(er[t]));
     }
     const int ev = tid >> 2, s = tid & 3;
     if (ev >= n) return;
@@ -230,6 +236,7 @@ __device__ __noinline__ void eig_values(const double *A, int n, double gl, doubl
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int jn = min(64, n - 64 * t);
+#pragma unroll 4
             for (int l = 0; l < jn; ++l) {
                 const double d = rl64(dr[t], l), e2 = rl64(er[t], l);
                 sturm_step(d, e2, x1, pivmin, p1, pm1, c1);
@@ -277,6 +284,7 @@ __device__ __noinline__ double eig_vectors(const double *A, const double *lamv, 
         const int idx = (j < n) ? pk_idx(j, j, n) : 0;
         dr[t] = (j < n) ? A[idx] : 0.0;
         er[t] = (j + 1 < n) ? A[idx + 1] : 0.0;
+        __asm__ volatile("" ::"v"(dr[t]), "v"(er[t]));   // loaded by every lane (see eig_values)
     }
     if (i >= n) return 0.0;
     const double lam = lamv[i];
