@@ -16,20 +16,20 @@
 #include <math.h>
 
 #include <algorithm>
+#include <utility>
 
 #include "lrs_common.h"
 
 namespace lrs {
 
-constexpr int kGramTile = 32;
-constexpr int kGramRows = 1024;   // rows per slab
-constexpr int kGramChunk = 64;    // rows staged per LDS chunk
+constexpr int kGramSlabs = 256;
+constexpr int kApSteps = 50;   // k-steps of 4 of the SVT apply: B <= 200
 constexpr int kJacobiThreads = 1024;
 constexpr int kMaxBp = 200;       // packed fp64 triangle of 200 x 200 = 160,800 B of LDS
 constexpr int kMaxSweeps = 40;
 
 struct SvtWs {
-    double *partial;  // [nslab][ntile_pairs][32*32]
+    double *partial;  // [kGramSlabs][16x16 tile pairs][256]  Gram partials
     double *G;        // [Bp][Bp]
     double *A0;       // [Bp][Bp]  V^T G V (warm start)
     double *T;        // [Bp][Bp]  scratch
@@ -39,18 +39,15 @@ struct SvtWs {
     double *beta;     // [Bp]      Householder scalars (tridiagonal path)
     double *F;        // [Bp][4][Bp] pivoted LU rows of T - lambda_i I (inverse iteration)
     float *E;         // [B][B]
+    float *Fp;        // [kApSteps][B][4]  I - E in the apply kernel's fragment order
     int *state;       // [0] V valid, [1] current V buffer, [2] rounds, [3] sweeps,
                       // [4] path of the last solve (1 tridiagonal, 2 Jacobi fallback, 3 Jacobi)
-    int64_t nslab, ntp, Bp;
+    int64_t Bp;
 };
 
-static inline int64_t gram_ntiles(int64_t B) { return (B + kGramTile - 1) / kGramTile; }
 
 static SvtWs svt_ws_layout(void *base, int64_t P, int64_t B) {
     SvtWs w;
-    const int64_t nt = gram_ntiles(B);
-    w.nslab = (P + kGramRows - 1) / kGramRows;
-    w.ntp = nt * (nt + 1) / 2;
     w.Bp = B + (B & 1);
     char *p = (char *)base;
     auto take = [&](size_t bytes) {
@@ -60,7 +57,7 @@ static SvtWs svt_ws_layout(void *base, int64_t P, int64_t B) {
     };
     const size_t mat = (size_t)w.Bp * w.Bp * sizeof(double);
     w.state = (int *)take(256);
-    w.partial = (double *)take((size_t)w.nslab * w.ntp * kGramTile * kGramTile * sizeof(double));
+    w.partial = (double *)take((size_t)kGramSlabs * 91 * 256 * sizeof(double));   // 91 = pairs of 13 blocks
     w.G = (double *)take(mat);
     w.A0 = (double *)take(mat);
     w.T = (double *)take(mat);
@@ -70,6 +67,7 @@ static SvtWs svt_ws_layout(void *base, int64_t P, int64_t B) {
     w.rot = (double *)take((size_t)kMaxSweeps * (w.Bp - 1) * (w.Bp / 2) * 2 * sizeof(double));
     w.beta = (double *)take((size_t)w.Bp * sizeof(double));
     w.F = (double *)take((size_t)4 * mat);
+    w.Fp = (float *)take((size_t)kApSteps * B * 4 * sizeof(float));
     w.E = (float *)take((size_t)B * B * sizeof(float));
     return w;
 }
@@ -94,76 +92,136 @@ __device__ __forceinline__ void rr_pair(int r, int k, int Bp, int &p, int &q) {
     if (p > q) { int t = p; p = q; q = t; }
 }
 
-// ---- 1. partial Gram over a slab of rows, one 32x32 upper-triangular tile pair per workgroup --
-__global__ __launch_bounds__(256) void k_gram_partial(const float *__restrict__ X, const float *__restrict__ L2,
-                                                      float c2, int64_t P, int B, int ntiles,
-                                                      double *__restrict__ partial) {
-    const int tp = blockIdx.x;   // tile pair index (ti <= tj)
-    const int slab = blockIdx.y;
-    int ti = 0, rem = tp;
-    while (rem >= ntiles - ti) { rem -= ntiles - ti; ++ti; }
-    const int tj = ti + rem;
-    __shared__ float Zi[kGramChunk][kGramTile + 1];
-    __shared__ float Zj[kGramChunk][kGramTile + 1];
-    const int tid = threadIdx.x;
-    const int oi = tid / 8;            // output row within tile  (0..31)
-    const int oj0 = (tid % 8) * 4;     // 4 output cols
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    const int64_t r_begin = (int64_t)slab * kGramRows;
-    const int64_t r_end = min<int64_t>(r_begin + kGramRows, P);
-    for (int64_t r0 = r_begin; r0 < r_end; r0 += kGramChunk) {
+// ---- 1. Gram G = Z^T Z on the fp64 matrix cores ---------------------------------------------
+// Z = X + c2*L2 (float32: exact in fp64).  One workgroup per slab of rows computes every 16 x 16
+// tile pair (a <= b) of the nt = ceil(B/16) column blocks, so Z is read from HBM once: rows are
+// staged kGramChunk at a time into LDS with float4 loads (Z formed on the way), then per k-step
+// of 4 rows a lane reads Z[p0 + (l>>4)][16c + (l&15)] for all nt blocks (the A and B fragments of
+// v_mfma_f64_16x16x4 have that same form) and wave w issues the MFMAs of pairs w, w + 4, ...
+// (compile-time pair lists: one instantiation per wave).  Partials [slab][pair][16*16] are
+// reduced in fixed order, so G is deterministic.
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+constexpr int kGramNt = 13, kGramPairs = kGramNt * (kGramNt + 1) / 2;   // B <= 208
+constexpr int kGramChunk = 32, kGramLd = 16 * kGramNt + 4;              // rows per LDS chunk, row stride
+constexpr int kGramBatch = 13;                                          // loads in flight per thread
+
+struct GramPairs {
+    int a[kGramPairs], b[kGramPairs];
+};
+__host__ __device__ constexpr GramPairs gram_pairs() {
+    GramPairs t{};
+    int k = 0;
+    for (int a = 0; a < kGramNt; ++a)
+        for (int b = a; b < kGramNt; ++b) {
+            t.a[k] = a;
+            t.b[k] = b;
+            ++k;
+        }
+    return t;
+}
+
+template <int PI>
+struct GramPair {
+    static constexpr int a = gram_pairs().a[PI], b = gram_pairs().b[PI];
+};
+
+template <int W, int... U>
+__device__ __forceinline__ void gram_mfmas(const double (&f)[kGramNt], doublex4 (&acc)[sizeof...(U)],
+                                           std::integer_sequence<int, U...>) {
+    ((acc[U] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[GramPair<W + 4 * U>::a], f[GramPair<W + 4 * U>::b], acc[U], 0,
+                                                    0, 0)),
+     ...);
+}
+
+// Whole workgroup body for wave W (every wave runs the same staging and barriers; the pair list,
+// the accumulators and their stores are compile-time per wave, so they stay in registers).
+template <int W>
+__device__ __forceinline__ void gram_body(float *Zs, const float *__restrict__ X, const float *__restrict__ L2,
+                                          float c2, int B, int64_t pbeg, int64_t pend, double *__restrict__ out) {
+    constexpr int NP = (kGramPairs - W + 3) / 4;
+    const int lane = threadIdx.x & 63, g = lane >> 4, jl = lane & 15;
+    doublex4 acc[NP];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) acc[u] = doublex4{0.0, 0.0, 0.0, 0.0};
+    for (int64_t c0 = pbeg; c0 < pend; c0 += kGramChunk) {
+        const int rows = (int)min<int64_t>(kGramChunk, pend - c0);
         __syncthreads();
-        for (int idx = tid; idx < kGramChunk * kGramTile; idx += 256) {
-            const int rr = idx / kGramTile, cc = idx % kGramTile;
-            const int64_t r = r0 + rr;
-            float zi = 0.f, zj = 0.f;
-            if (r < r_end) {
-                const int ci = ti * kGramTile + cc, cj = tj * kGramTile + cc;
-                if (ci < B) {
-                    zi = X[r * B + ci];
-                    if (L2) zi = zi + c2 * L2[r * B + ci];   // X + (1/mu_2)*lambda_2
-                }
-                if (cj < B) {
-                    zj = X[r * B + cj];
-                    if (L2) zj = zj + c2 * L2[r * B + cj];
+        // rows x B elements, kGramBatch loads in flight per thread, then the LDS stores
+        for (int e0 = threadIdx.x; e0 < kGramChunk * B; e0 += 256 * kGramBatch) {
+            float z[kGramBatch];
+#pragma unroll
+            for (int u = 0; u < kGramBatch; ++u) {
+                const int e = e0 + 256 * u, rr = e / B;
+                z[u] = 0.f;
+                if (e < kGramChunk * B && rr < rows) {
+                    const int64_t o = c0 * B + e;
+                    z[u] = X[o];
+                    if (L2) z[u] = z[u] + c2 * L2[o];   // X + (1/mu_2)*lambda_2
                 }
             }
-            Zi[rr][cc] = zi;
-            Zj[rr][cc] = zj;
+#pragma unroll
+            for (int u = 0; u < kGramBatch; ++u) {
+                const int e = e0 + 256 * u, rr = e / B, c = e - rr * B;
+                if (e < kGramChunk * B) Zs[rr * kGramLd + c] = z[u];
+            }
+        }
+        for (int idx = threadIdx.x; idx < kGramChunk * (kGramLd - B); idx += 256) {   // zero pad columns
+            const int rr = idx / (kGramLd - B), c = B + idx % (kGramLd - B);
+            Zs[rr * kGramLd + c] = 0.f;
         }
         __syncthreads();
-#pragma unroll 8
-        for (int rr = 0; rr < kGramChunk; ++rr) {
-            const double a = (double)Zi[rr][oi];
+        const int rows4 = (rows + 3) & ~3;
+        for (int r = 0; r < rows4; r += 4) {
+            double f[kGramNt];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k] = __fma_rn(a, (double)Zj[rr][oj0 + k], acc[k]);
+            for (int c = 0; c < kGramNt; ++c) f[c] = (double)Zs[(r + g) * kGramLd + 16 * c + jl];
+            gram_mfmas<W>(f, acc, std::make_integer_sequence<int, NP>{});
         }
     }
-    double *out = partial + ((int64_t)slab * gridDim.x + tp) * (kGramTile * kGramTile);
+    // C/D layout of the f64 MFMA: column l & 15, row (l >> 4) + 4 r
 #pragma unroll
-    for (int k = 0; k < 4; ++k) out[oi * kGramTile + oj0 + k] = acc[k];
+    for (int u = 0; u < NP; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(int64_t)(W + 4 * u) * 256 + (g + 4 * r) * 16 + jl] = acc[u][r];
+}
+
+__global__ __launch_bounds__(256, 1) void k_gram_mfma(const float *__restrict__ X, const float *__restrict__ L2,
+                                                      float c2, int64_t P, int B, int64_t rows_per_slab,
+                                                      double *__restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float Zs[kGramChunk * kGramLd];
+    const int sl = blockIdx.x, wv = threadIdx.x >> 6;
+    const int64_t pbeg = (int64_t)sl * rows_per_slab, pend = min<int64_t>(P, pbeg + rows_per_slab);
+    double *out = partial + (int64_t)sl * kGramPairs * 256;
+    switch (wv) {
+    case 0: gram_body<0>(Zs, X, L2, c2, B, pbeg, pend, out); break;
+    case 1: gram_body<1>(Zs, X, L2, c2, B, pbeg, pend, out); break;
+    case 2: gram_body<2>(Zs, X, L2, c2, B, pbeg, pend, out); break;
+    default: gram_body<3>(Zs, X, L2, c2, B, pbeg, pend, out); break;
+    }
 }
 
 // ---- 1b. fixed-order reduction of the slab partials into the full symmetric Gram ------------
-__global__ __launch_bounds__(256) void k_gram_reduce(const double *__restrict__ partial, int64_t nslab, int ntp,
-                                                     int ntiles, int B, int Bp, double *__restrict__ G) {
-    const int64_t total = (int64_t)ntp * kGramTile * kGramTile;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int tp = (int)(idx / (kGramTile * kGramTile));
-        const int e = (int)(idx % (kGramTile * kGramTile));
-        int ti = 0, rem = tp;
-        while (rem >= ntiles - ti) { rem -= ntiles - ti; ++ti; }
-        const int tj = ti + rem;
-        const int i = ti * kGramTile + e / kGramTile, j = tj * kGramTile + e % kGramTile;
-        double s = 0.0;
-        for (int64_t sl = 0; sl < nslab; ++sl) s += partial[(sl * ntp + tp) * (kGramTile * kGramTile) + e];
-        if (i < Bp && j < Bp) {
-            const double v = (i < B && j < B) ? s : 0.0;   // pad row/col (B odd) is zero
-            G[(int64_t)i * Bp + j] = v;
-            G[(int64_t)j * Bp + i] = v;
-        }
+__global__ __launch_bounds__(256) void k_gram_reduce16(const double *__restrict__ partial, int nslab, int nt, int B,
+                                                       int Bp, double *__restrict__ G) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)Bp * Bp) return;
+    const int i = (int)(idx / Bp), j = (int)(idx % Bp);
+    if (j < i) return;
+    double s = 0.0;
+    if (i < B && j < B) {
+        const int a = i >> 4, b = j >> 4, npair = kGramPairs;
+        const int pi = a * kGramNt - ((a * (a - 1)) >> 1) + (b - a);
+        const int e = (i & 15) * 16 + (j & 15);
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int sl = 0;
+        for (; sl + 8 <= nslab; sl += 8)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += partial[((int64_t)(sl + u) * npair + pi) * 256 + e];
+        for (; sl < nslab; ++sl) acc[sl & 7] += partial[((int64_t)sl * npair + pi) * 256 + e];
+        s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
+    G[(int64_t)i * Bp + j] = s;   // pad row/col (B odd) is zero
+    G[(int64_t)j * Bp + i] = s;
 }
 
 // ---- 2. warm start A0 = V^T (G V) with the current V (16 x 16 fp64 tiles) -------------------
@@ -495,7 +553,7 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double 
         w.state[4] = bad ? 2 : 1;
     }
     __syncthreads();
-    eig_syrk<false, 0>(sm, w.V[cur], n, w.lam, tau, B, w.E, nullptr, red);
+    eig_syrk<false, 0>(sm, w.V[cur], n, w.lam, tau, B, w.E, nullptr, red, w.Fp);
     if (tid == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -526,7 +584,10 @@ __global__ __launch_bounds__(256) void k_build_E(SvtWs w, int B, double tau) {
         for (int k = 0; k < 16; ++k) acc = __fma_rn(Vi[ty][k] * ek[k], Vj[tx][k], acc);
         __syncthreads();
     }
-    if (i < B && j < B) w.E[(int64_t)i * B + j] = (float)acc;
+    if (i < B && j < B) {
+        w.E[(int64_t)i * B + j] = (float)acc;
+        store_fp(w.Fp, B, i, j, (float)acc);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_sorted_singular_values(SvtWs w, int B, double *__restrict__ s_out) {
@@ -543,156 +604,77 @@ __global__ __launch_bounds__(256) void k_sorted_singular_values(SvtWs w, int B, 
     }
 }
 
-// ---- 5b'. U = Z - Z E on the bf16 matrix cores (B <= 224) -----------------------------------
-// Operands split exactly into three bf16 terms, six partial products (fp32-GEMM accuracy), so
-// the product leaves the VALU, which the concurrently running sparse-coding kernel saturates.
-// grid (row groups, column chunks of 64): each workgroup stages its 64 columns of E once (three
-// bf16 images [col][k], 464-B rows: conflict-free ds_read_b128) and loops over row blocks of 64;
-// wave w owns rows 16w..16w+15 of a block, 4 column tiles.
-typedef __bf16 sbf16x8 __attribute__((ext_vector_type(8)));
-constexpr int kApKMax = 224, kApLd = 232, kApCols = 64;
+// ---- 5b. U = Z (I - E) on the f32 matrix cores --------------------------------------------------
+// One wave per 16 rows and every column (ceil(B/16) <= 13 accumulator tiles), K walked in 50
+// k-steps of 4 (B <= 200).  The k-steps are ordered so that a lane's two A values of k-steps 2q,
+// 2q+1 are one aligned float2 of its Z row (k = 8q + 2g + h, lane group g = l >> 4), and F = I - E
+// was written in that order by the eigensolver (Fp, store_fp): each B fragment is 64 consecutive
+// floats out of L2.  No LDS, so several waves per SIMD hide the memory latency; Z is read once and
+// U written once.  Exact f32 products, fp32 accumulation.
+constexpr int kApTiles = 13, kApRows = 1;   // accumulator tiles per wave: 16 kApRows rows x 13 x 16 columns
 
-__device__ __forceinline__ void ap_split3(float v, __bf16 &a, __bf16 &b, __bf16 &c) {
-    a = (__bf16)v;
-    const float r1 = v - (float)a;
-    b = (__bf16)r1;
-    c = (__bf16)(r1 - (float)b);
-}
-
-__device__ __forceinline__ floatx4 ap_mfma(const sbf16x8 &a, const sbf16x8 &b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-__global__ __launch_bounds__(256) void k_svt_apply_b3(const float *__restrict__ X, const float *__restrict__ L2,
-                                                      float c2, const float *__restrict__ E, int64_t P, int B,
-                                                      float *__restrict__ U) {
-    extern __shared__ __align__(16) __bf16 Es[];   // [3][kApCols][kApLd]
-    const int c0 = blockIdx.y * kApCols;
-    for (int idx = threadIdx.x; idx < kApCols * kApKMax; idx += 256) {
-        const int cc = idx / kApKMax, k = idx % kApKMax;
-        const int c = c0 + cc;
-        const float v = (k < B && c < B) ? E[(int64_t)k * B + c] : 0.0f;
-        __bf16 a, b, d;
-        ap_split3(v, a, b, d);
-        Es[(0 * kApCols + cc) * kApLd + k] = a;
-        Es[(1 * kApCols + cc) * kApLd + k] = b;
-        Es[(2 * kApCols + cc) * kApLd + k] = d;
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int jl = lane & 15, g = lane >> 4;
-    const int nks = (B + 31) / 32;
-    for (int64_t rb = (int64_t)blockIdx.x * 64; rb < P; rb += (int64_t)gridDim.x * 64) {
-        const int64_t row = rb + 16 * w + jl;            // A-operand row of this lane
-        floatx4 acc[4];
+template <int RT>
+__global__ __launch_bounds__(256) void k_svt_apply_f(const float *__restrict__ X, const float *__restrict__ L2,
+                                                     float c2, const float *__restrict__ Fp, int64_t P, int B,
+                                                     float *__restrict__ U) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, jl = lane & 15;
+    const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (16 * RT);
+    if (r0 >= P) return;
+    floatx4 acc[RT][kApTiles];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-        for (int ks = 0; ks < nks; ++ks) {
-            const int kb = 32 * ks + 8 * g;
-            sbf16x8 A[3];
+    for (int m = 0; m < RT; ++m)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = kb + j;
-                float z = 0.0f;
-                if (row < P && k < B) {
-                    z = X[row * B + k];
-                    if (L2) z = z + c2 * L2[row * B + k];
+        for (int t = 0; t < kApTiles; ++t) acc[m][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int q = 0; q < kApSteps / 2; ++q) {
+        const int k = 8 * q + 2 * g;
+        float2 z[RT];
+#pragma unroll
+        for (int m = 0; m < RT; ++m) {
+            const int64_t row = r0 + 16 * m + jl;
+            z[m] = make_float2(0.f, 0.f);
+            if (row < P && k < B) {
+                if ((B & 1) == 0) {   // even B: 8-byte aligned rows, k + 1 < B
+                    z[m] = *reinterpret_cast<const float2 *>(&X[row * B + k]);
+                    if (L2) {
+                        const float2 l = *reinterpret_cast<const float2 *>(&L2[row * B + k]);
+                        z[m].x = z[m].x + c2 * l.x;   // X + (1/mu_2)*lambda_2
+                        z[m].y = z[m].y + c2 * l.y;
+                    }
+                } else {
+                    z[m].x = X[row * B + k];
+                    if (L2) z[m].x = z[m].x + c2 * L2[row * B + k];
+                    if (k + 1 < B) {
+                        z[m].y = X[row * B + k + 1];
+                        if (L2) z[m].y = z[m].y + c2 * L2[row * B + k + 1];
+                    }
                 }
-                __bf16 a, b, d;
-                ap_split3(z, a, b, d);
-                A[0][j] = a; A[1][j] = b; A[2][j] = d;
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int cc = 16 * t + jl;
-                sbf16x8 Bf[3];
-#pragma unroll
-                for (int sp = 0; sp < 3; ++sp)
-                    Bf[sp] = *reinterpret_cast<const sbf16x8 *>(&Es[(sp * kApCols + cc) * kApLd + kb]);
-                floatx4 a4 = acc[t];
-                a4 = ap_mfma(A[2], Bf[0], a4);
-                a4 = ap_mfma(A[1], Bf[1], a4);
-                a4 = ap_mfma(A[0], Bf[2], a4);
-                a4 = ap_mfma(A[1], Bf[0], a4);
-                a4 = ap_mfma(A[0], Bf[1], a4);
-                a4 = ap_mfma(A[0], Bf[0], a4);
-                acc[t] = a4;
             }
         }
-        // C layout: rows 4g + i of the wave's 16, column jl of tile t
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int c = c0 + 16 * t + jl;
+        for (int h = 0; h < 2; ++h) {
+            const float *fb = Fp + (int64_t)(2 * q + h) * B * 4 + g;
+#pragma unroll
+            for (int t = 0; t < kApTiles; ++t) {
+                const int c = 16 * t + jl;
+                const float b = c < B ? fb[c * 4] : 0.0f;
+#pragma unroll
+                for (int m = 0; m < RT; ++m) acc[m][t] = mfma16x16x4(h ? z[m].y : z[m].x, b, acc[m][t]);
+            }
+        }
+    }
+    // acc[m][t][i] = U[r0 + 16m + 4g + i][16t + jl]
+#pragma unroll
+    for (int m = 0; m < RT; ++m)
+#pragma unroll
+        for (int t = 0; t < kApTiles; ++t) {
+            const int c = 16 * t + jl;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int64_t r = rb + 16 * w + 4 * g + i;
-                if (r < P && c < B) {
-                    float z = X[r * B + c];
-                    if (L2) z = z + c2 * L2[r * B + c];
-                    U[r * B + c] = z - acc[t][i];
-                }
+                const int64_t r = r0 + 16 * m + 4 * g + i;
+                if (r < P && c < B) U[r * B + c] = acc[m][t][i];
             }
         }
-    }
-}
-
-// ---- 5b. U = Z - Z E  (64 x 64 output tile per workgroup, f32) ------------------------------
-constexpr int kAT = 64;   // output tile
-constexpr int kAK = 16;   // k chunk
-
-__global__ __launch_bounds__(256) void k_svt_apply(const float *__restrict__ X, const float *__restrict__ L2, float c2,
-                                                   const float *__restrict__ E, int64_t P, int B,
-                                                   float *__restrict__ U) {
-    __shared__ float Zs[kAK][kAT + 1];   // [k][row]
-    __shared__ float Es[kAK][kAT + 1];   // [k][col]
-    const int64_t r0 = (int64_t)blockIdx.x * kAT;
-    const int c0 = blockIdx.y * kAT;
-    const int tid = threadIdx.x;
-    const int tr = tid / 16, tc = tid % 16;  // 4x4 outputs per thread
-    float acc[4][4] = {};
-    for (int k0 = 0; k0 < B; k0 += kAK) {
-        __syncthreads();
-        for (int idx = tid; idx < kAK * kAT; idx += 256) {
-            const int rr = idx / kAK, kk = idx % kAK;
-            const int64_t r = r0 + rr;
-            const int k = k0 + kk;
-            float z = 0.f;
-            if (r < P && k < B) {
-                z = X[r * B + k];
-                if (L2) z = z + c2 * L2[r * B + k];
-            }
-            Zs[kk][rr] = z;
-            const int kk2 = idx / kAT, cc = idx % kAT;
-            const int k2 = k0 + kk2, c = c0 + cc;
-            Es[kk2][cc] = (k2 < B && c < B) ? E[(int64_t)k2 * B + c] : 0.f;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int kk = 0; kk < kAK; ++kk) {
-            float a[4], b[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = Zs[kk][tr * 4 + i];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) b[i] = Es[kk][tc * 4 + i];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) acc[i][jj] = __fmaf_rn(a[i], b[jj], acc[i][jj]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int64_t r = r0 + tr * 4 + i;
-        if (r >= P) continue;
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int c = c0 + tc * 4 + jj;
-            if (c >= B) continue;
-            float z = X[r * B + c];
-            if (L2) z = z + c2 * L2[r * B + c];
-            U[r * B + c] = z - acc[i][jj];
-        }
-    }
 }
 
 }  // namespace lrs
@@ -704,7 +686,7 @@ extern "C" size_t lrs_svt_workspace(int64_t P, int64_t B) {
     return svt_ws_bytes(P, B);
 }
 
-// Stage 1 (multi-workgroup, ~0.3 ms): fp64 Gram and, when warm, A0 = V^T G V.
+// Stage 1 (multi-workgroup): fp64 Gram on the matrix cores and, for a warm Jacobi, A0 = V^T G V.
 extern "C" int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, int warm, void *ws,
                                 size_t ws_bytes, void *stream) {
     if (!X || !ws || P <= 0 || B <= 0) return LRS_E_INVALID;
@@ -716,14 +698,13 @@ extern "C" int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64
         hipError_t e = hipMemsetAsync(w.state, 0, sizeof(int) * 4, st);
         if (e != hipSuccess) return (int)e;
     }
-    const int nt = (int)gram_ntiles(B);
     const int Bp = (int)w.Bp;
-    hipLaunchKernelGGL(k_gram_partial, dim3((unsigned)w.ntp, (unsigned)w.nslab), dim3(256), 0, st, X, L2, c2, P,
-                       (int)B, nt, w.partial);
+    int64_t rows = ((P + kGramSlabs - 1) / kGramSlabs + 3) / 4 * 4;
+    const int nslab = (int)((P + rows - 1) / rows);
+    hipLaunchKernelGGL(k_gram_mfma, dim3((unsigned)nslab), dim3(256), 0, st, X, L2, c2, P, (int)B, rows, w.partial);
     LRS_CHECK_LAUNCH();
-    const int64_t tot = w.ntp * kGramTile * kGramTile;
-    hipLaunchKernelGGL(k_gram_reduce, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 4096)), dim3(256), 0, st,
-                       w.partial, w.nslab, (int)w.ntp, nt, (int)B, Bp, w.G);
+    hipLaunchKernelGGL(k_gram_reduce16, dim3((unsigned)((Bp * Bp + 255) / 256)), dim3(256), 0, st, w.partial, nslab,
+                       kGramNt, (int)B, Bp, w.G);
     LRS_CHECK_LAUNCH();
     if ((warm & LRS_SVT_WARM) && (warm & LRS_SVT_JACOBI)) {
         // A0 = V^T (G V) with the current V (unused when V is not valid yet: Jacobi starts from G)
@@ -781,19 +762,8 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
         hipLaunchKernelGGL(k_sorted_singular_values, dim3(1), dim3(256), 0, st, w, (int)B, s_out);
         LRS_CHECK_LAUNCH();
     }
-    if (B <= kApKMax) {
-        const size_t lds = sizeof(__bf16) * 3 * kApCols * kApLd;
-        hipError_t e = hipFuncSetAttribute((const void *)k_svt_apply_b3, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds);
-        if (e != hipSuccess) return (int)e;
-        int64_t rgroups = (P + 63) / 64;
-        if (rgroups > 64) rgroups = 64;
-        dim3 grid((unsigned)rgroups, (unsigned)((B + kApCols - 1) / kApCols));
-        hipLaunchKernelGGL(k_svt_apply_b3, grid, dim3(256), lds, st, X, L2, c2, w.E, P, (int)B, U);
-    } else {
-        dim3 grid((unsigned)((P + kAT - 1) / kAT), (unsigned)((B + kAT - 1) / kAT));
-        hipLaunchKernelGGL(k_svt_apply, grid, dim3(256), 0, st, X, L2, c2, w.E, P, (int)B, U);
-    }
+    hipLaunchKernelGGL(k_svt_apply_f<kApRows>, dim3((unsigned)((P + 64 * kApRows - 1) / (64 * kApRows))), dim3(256), 0,
+                       st, X, L2, c2, w.Fp, P, (int)B, U);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -833,10 +803,28 @@ extern "C" int lrs_diag_svt_eig(void *ws, int64_t P, int64_t B, double *out, voi
     e = hipMemcpy(state, w.state, sizeof(state), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return (int)e;
     const size_t m = (size_t)Bp * Bp;
-    hipMemcpy(out, w.partial, 2 * Bp * sizeof(double), hipMemcpyDeviceToHost);
-    hipMemcpy(out + 2 * Bp, w.lam, Bp * sizeof(double), hipMemcpyDeviceToHost);
-    hipMemcpy(out + 3 * Bp, w.T, m * sizeof(double), hipMemcpyDeviceToHost);
-    hipMemcpy(out + 3 * Bp + m, w.V[state[1]], m * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(out, w.partial, 2 * Bp * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(out + 2 * Bp, w.lam, Bp * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(out + 3 * Bp, w.T, m * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(out + 3 * Bp + m, w.V[state[1]], m * sizeof(double), hipMemcpyDeviceToHost);
     e = hipMemcpy(out + 3 * Bp + 2 * m, w.A0, m * sizeof(double), hipMemcpyDeviceToHost);
     return e != hipSuccess ? (int)e : state[4];
+}
+
+// Diagnostics: the SVT apply alone (F = I - E from the last solve in ws).
+extern "C" int lrs_diag_svt_apply(const float *X, const float *L2, float c2, int64_t P, int64_t B, void *ws, float *U,
+                                  int dbg, void *stream) {
+    SvtWs w = svt_ws_layout(ws, P, B);
+    hipStream_t st = (hipStream_t)stream;
+    if (dbg == 1)
+        hipLaunchKernelGGL(k_svt_apply_f<1>, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, st, X, L2, c2, w.Fp, P,
+                           (int)B, U);
+    else if (dbg == 2)
+        hipLaunchKernelGGL(k_svt_apply_f<2>, dim3((unsigned)((P + 127) / 128)), dim3(256), 0, st, X, L2, c2, w.Fp, P,
+                           (int)B, U);
+    else
+        hipLaunchKernelGGL(k_svt_apply_f<4>, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, X, L2, c2, w.Fp, P,
+                           (int)B, U);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
 }

@@ -430,6 +430,14 @@ __device__ __noinline__ void eig_backtransform(const double *A, const double *bl
     }
 }
 
+// F = I - E in the layout of the SVT apply kernel's MFMA B fragments: K is walked in k-steps
+// st = 2q + h whose lane group g holds k = 8q + 2g + h (so a lane's two A values of a q are one
+// aligned float2 of a Z row); Fp[(st * B + c) * 4 + g] = F[k][c].
+__device__ __forceinline__ void store_fp(float *Fp, int B, int k, int c, float e) {
+    const int q = k >> 3, g = (k >> 1) & 3, h = k & 1, st = 2 * q + h;
+    Fp[((int64_t)st * B + c) * 4 + g] = (k == c ? 1.0f : 0.0f) - e;
+}
+
 // ---- one-workgroup fp64 products on a 32 x 32 thread grid -------------------------------------
 // Operands staged kEKc values of the summation index at a time as [kk][row] images (row stride
 // kELd = 225 doubles: the transposed staging stores hit distinct banks).  Thread (ty, tx) owns
@@ -466,7 +474,7 @@ __device__ __forceinline__ void eig_stage(double *Xs, const double *X, int ld, i
 // MODE 1: f = 1, C -> S (double, n x n) and the return value is max |S - I| (uniform).
 template <bool KMAJ, int MODE>
 __device__ __noinline__ double eig_syrk(double *sm, const double *X, int n, const double *lam, double tau, int B,
-                                        float *E, double *S, double *red) {
+                                        float *E, double *S, double *red, float *Fp = nullptr) {
     double *Xs = sm;                   // [kEKc][kELd]
     double *Xf = sm + kEKc * kELd;     // [kEKc][kELd]  X * f  (MODE 0)
     const int tid = threadIdx.x, ty = tid >> 5, tx = tid & 31;
@@ -518,8 +526,11 @@ __device__ __noinline__ double eig_syrk(double *sm, const double *X, int n, cons
             const int lim = MODE == 0 ? B : n;
             if (i < lim && j < lim && (a != b || tx >= ty)) {
                 if (MODE == 0) {
-                    E[(int64_t)i * B + j] = (float)acc[a][b];
-                    E[(int64_t)j * B + i] = (float)acc[a][b];
+                    const float e = (float)acc[a][b];
+                    E[(int64_t)i * B + j] = e;
+                    E[(int64_t)j * B + i] = e;
+                    store_fp(Fp, B, i, j, e);
+                    store_fp(Fp, B, j, i, e);
                 } else {
                     S[(int64_t)i * n + j] = acc[a][b];
                     S[(int64_t)j * n + i] = acc[a][b];
