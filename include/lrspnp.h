@@ -44,6 +44,7 @@ extern "C" {
 #define LRS_ALPHA_SOFT 2  /* alpha = ||H||_2^2, soft threshold T (ista.m:15-23)              */
 #define LRS_PROX_NLM 0
 #define LRS_PROX_SOFT 1
+#define LRS_PROX_NLM_MATLAB 2 /* NLmeansfilter(g,3,3,0.1T) of pnp_ista.m:30, fp64        */
 
 const char *lrs_version(void);
 /* 0 when the current device is gfx950, LRS_E_NODEVICE otherwise. */

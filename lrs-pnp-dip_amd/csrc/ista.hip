@@ -215,6 +215,94 @@ __device__ __forceinline__ void nlm_prox_registers(const floatx4 (&G)[K / 16], f
     }
 }
 
+// MATLAB-variant prox (LRS-PnP(Matlab Code)/pnp_ista.m:30: NLmeansfilter(gradient, 3, 3, 0.1 T),
+// NLmeansfilter.m:18-78), fp64, along the atom axis: 'symmetric' padding, a 7-row similarity
+// window weighted by the row sums krow of make_kernel(3), exp(-d/h^2) weights over the 6 nearest
+// atoms, the centre weighted by the largest of them.  A chunk of 4 atoms needs atoms a-6 .. a+9:
+// chunks c-2 .. c+2, i.e. lanes l-32 .. l+32 of tiles q-1 .. q+1.  Same evaluation order as
+// oracle/nlm_oracle.c:oracle_nlm_matlab_col.
+__device__ __forceinline__ void nlm_matlab_krow(double (&krow)[7]) {
+#pragma unroll
+    for (int u = -3; u <= 3; ++u) {
+        const int a = u < 0 ? -u : u;
+        double s = 0.0;
+        for (int d = (a < 1 ? 1 : a); d <= 3; ++d) s = s + 1.0 / (double)(2 * d + 1);
+        krow[u + 3] = s / 3.0;
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void nlm_matlab_prox_registers(const floatx4 (&G)[K / 16], float (&X)[K / 16][4],
+                                                          double h, int lane) {
+    constexpr int NQ = K / 16, NC = K / 4;
+    const int g = lane >> 4;
+    const int p1 = (lane + 48) & 63, p2 = (lane + 32) & 63, n1 = (lane + 16) & 63;
+    double krow[7];
+    nlm_matlab_krow(krow);
+    const double h2 = h * h;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int qp = q > 0 ? q - 1 : 0, qn = q + 1 < NQ ? q + 1 : NQ - 1;
+        float w[16];
+        // chunk c-2 (last two atoms), c-1, own, c+1, c+2 (first two atoms)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float cur = __shfl(G[q][2 + e], p2, 64), prv = __shfl(G[qp][2 + e], p2, 64);
+            w[e] = g >= 2 ? cur : prv;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float cur = __shfl(G[q][e], p1, 64), prv = __shfl(G[qp][e], p1, 64);
+            w[2 + e] = g >= 1 ? cur : prv;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[6 + e] = G[q][e];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float cur = __shfl(G[q][e], n1, 64), nxt = __shfl(G[qn][e], n1, 64);
+            w[10 + e] = g <= 2 ? cur : nxt;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float cur = __shfl(G[q][e], p2, 64), nxt = __shfl(G[qn][e], p2, 64);
+            w[14 + e] = g <= 1 ? cur : nxt;
+        }
+        // symmetric padding: g-hat[j] = g[-j-1] (j < 0), g[2K-1-j] (j >= K)
+        const int c = 4 * q + g;
+        if (c == 0) { w[2] = w[9]; w[3] = w[8]; w[4] = w[7]; w[5] = w[6]; }
+        if (c == 1) { w[0] = w[3]; w[1] = w[2]; }
+        if (c == NC - 1) { w[10] = w[9]; w[11] = w[8]; w[12] = w[7]; w[13] = w[6]; }
+        if (c == NC - 2) { w[14] = w[13]; w[15] = w[12]; }
+        double v[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] = (double)w[e];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int i = 4 * c + e, p = 6 + e;
+            double sw = 0.0, av = 0.0, wmax = 0.0;
+#pragma unroll
+            for (int t = -3; t <= 3; ++t) {
+                if (t == 0) continue;
+                const int r = i + t;
+                if (r < 0 || r >= K) continue;
+                double d = 0.0;
+#pragma unroll
+                for (int u = -3; u <= 3; ++u) {
+                    const double df = v[p + u] - v[p + t + u];
+                    d = d + krow[u + 3] * (df * df);
+                }
+                const double wt = exp(-d / h2);
+                if (wt > wmax) wmax = wt;
+                sw = sw + wt;
+                av = av + wt * v[p + t];
+            }
+            av = av + wmax * v[p];
+            sw = sw + wmax;
+            X[q][e] = sw > 0.0 ? (float)(av / sw) : w[p];
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Resident kernel (n_pad <= 64, i.e. bb <= 8): dictionary in LDS for the whole launch, y and the
 // row mask in VGPRs, and a software pipeline over the 16 atom tiles q of each inner iteration:
@@ -1500,6 +1588,8 @@ __global__ __launch_bounds__(kIstaThreads, 2) void k_ista(IstaParams p) {
                     X[q][i] = gv > 0.f ? t : (gv < 0.f ? -t : 0.f);
                 }
             }
+        } else if (p.prox == LRS_PROX_NLM_MATLAB) {
+            nlm_matlab_prox_registers<K>(G, X, thr, lane);
         } else {
             nlm_prox_registers<K>(G, X, thr, lane);
         }
@@ -1584,7 +1674,7 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
                             int Nit, int prox, float *coefs, float *phi, void *stream) {
     if (!Yb || !obs || !D || !alpha || !thr || !phi || n <= 0 || nb < 0 || Nit < 0) return LRS_E_INVALID;
     if (n_pad % 16 != 0 || n_pad < n) return LRS_E_INVALID;
-    if (prox != LRS_PROX_NLM && prox != LRS_PROX_SOFT) return LRS_E_INVALID;
+    if (prox != LRS_PROX_NLM && prox != LRS_PROX_SOFT && prox != LRS_PROX_NLM_MATLAB) return LRS_E_INVALID;
     if (K != 256) return LRS_E_UNSUPPORTED;
     if (nb == 0) return LRS_OK;
     if (n_pad > (int64_t)1 << 20 || nb > ((int64_t)1 << 40)) return LRS_E_INVALID;
@@ -1594,7 +1684,9 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     hipStream_t st = (hipStream_t)stream;
     const bool split = g_ista_precision == LRS_ISTA_SPLIT_BF16;
     const dim3 grid_b3((unsigned)((nb + kB3Waves * 16 - 1) / (kB3Waves * 16)));
-    if (n_pad <= kStageRows && split && prox == LRS_PROX_SOFT)
+    if (prox == LRS_PROX_NLM_MATLAB)   // the MATLAB-variant prox lives in the streaming kernel only
+        hipLaunchKernelGGL((k_ista<256, false>), grid, dim3(kIstaThreads), 0, st, p);
+    else if (n_pad <= kStageRows && split && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_b3<256, true>), grid_b3, dim3(kB3Threads), 0, st, p);
     else if (n_pad <= kStageRows && split)
         hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, 1>), grid_b3, dim3(kB3Threads), 0, st, p);
@@ -1665,6 +1757,34 @@ extern "C" int lrs_diag_ista_ablate_f32(const float *Yb, const uint8_t *obs, con
     if (ablate == 1) hipLaunchKernelGGL((k_ista_res<256, false, 1>), grid, dim3(kIstaThreads), 0, st, p);
     else if (ablate == 2) hipLaunchKernelGGL((k_ista_res<256, false, 2>), grid, dim3(kIstaThreads), 0, st, p);
     else hipLaunchKernelGGL((k_ista_res<256, false, 0>), grid, dim3(kIstaThreads), 0, st, p);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+// Diagnostics: the in-register MATLAB-variant prox alone on [nb][256] vectors (16 per wave).
+__global__ __launch_bounds__(64) void k_diag_nlm_matlab(const float *__restrict__ g, const double *__restrict__ h,
+                                                       int64_t nb, float *__restrict__ out) {
+    constexpr int K = 256, NQ = K / 16;
+    const int lane = threadIdx.x, jl = lane & 15, gq = lane >> 4;
+    const int64_t j = (int64_t)blockIdx.x * 16 + jl;
+    const bool valid = j < nb;
+    floatx4 G[NQ];
+    float X[NQ][4];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) G[q][i] = valid ? g[j * K + 16 * q + 4 * gq + i] : 0.f;
+    nlm_matlab_prox_registers<K>(G, X, valid ? h[j] : 1.0, lane);
+    if (valid)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) out[j * K + 16 * q + 4 * gq + i] = X[q][i];
+}
+
+extern "C" int lrs_diag_nlm_matlab(const float *g, const double *h, int64_t nb, float *out, void *stream) {
+    hipLaunchKernelGGL(k_diag_nlm_matlab, dim3((unsigned)((nb + 15) / 16)), dim3(64), 0, (hipStream_t)stream, g, h,
+                       nb, out);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }

@@ -16,7 +16,7 @@ LRS_OK = 0
 LRS_E = {-1: "LRS_E_INVALID", -2: "LRS_E_UNSUPPORTED", -3: "LRS_E_WORKSPACE", -4: "LRS_E_NODEVICE"}
 
 ALPHA_SPEC2, ALPHA_FRO4, ALPHA_SOFT = 0, 1, 2
-PROX_NLM, PROX_SOFT = 0, 1
+PROX_NLM, PROX_SOFT, PROX_NLM_MATLAB = 0, 1, 2
 
 
 class LrsError(RuntimeError):

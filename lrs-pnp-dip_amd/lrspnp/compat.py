@@ -106,6 +106,13 @@ def ista_lip(y, H, lambda_ista, alpha, Nit):
     return _ista(y, H, lambda_ista, Nit, ops.ALPHA_FRO4, ops.PROX_NLM)
 
 
+def pnp_ista(y, H, lambda_ista, alpha, Nit, noise_sigma=None):
+    """pnp_ista.m (LRS-PnP Matlab Code/pnp_ista.m:1-32): alpha = max eig(H^T H) (= ||H||_2^2, the
+    value main_LRS_PnP.m passes), T = lambda/(2 alpha), x = NLmeansfilter(gradient, 3, 3, 0.1 T)
+    (NLmeansfilter.m).  The returned J (objective) of the MATLAB function is not computed."""
+    return _ista(y, H, lambda_ista, Nit, ops.ALPHA_SPEC2, ops.PROX_NLM_MATLAB)
+
+
 def ista_soft(y, H, lambda_ista, alpha, Nit):
     """ista.m (LRS-PnP Matlab Code/ista.m:1-24): alpha = norm(H)^2, soft threshold T."""
     return _ista(y, H, lambda_ista, Nit, ops.ALPHA_SOFT, ops.PROX_SOFT)

@@ -10,11 +10,12 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import (ALPHA_FRO4, ALPHA_SOFT, ALPHA_SPEC2, PROX_NLM, PROX_SOFT, LrsError, check,
+from ._lib import (ALPHA_FRO4, ALPHA_SOFT, ALPHA_SPEC2, PROX_NLM, PROX_NLM_MATLAB, PROX_SOFT, LrsError, check,
                    device_lib, lib)
 
 __all__ = ["nlm_col", "block_grid", "cover_ranges", "im2col", "ista_alpha", "ista", "svt_workspace",
-           "svt", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT"]
+           "svt", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT",
+           "PROX_NLM_MATLAB"]
 
 
 def _p(t):

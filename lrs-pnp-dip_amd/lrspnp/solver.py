@@ -30,7 +30,7 @@ class LrsPnPConfig:
     Nit: int = 80                 # inner ISTA iterations               :226
     bb: int = 36                  # block size                          :237
     sliding: int = 36             # slidingDis                          :238
-    variant: str = "spec2"        # 'spec2' (main), 'fro4' (DIP mains), 'soft' (ista.m)
+    variant: str = "spec2"        # 'spec2' (main), 'fro4' (DIP mains), 'soft' (ista.m), 'matlab' (pnp_ista.m)
     svt_method: str = "tri"       # SVT eigensolver: 'tri' (tridiagonal, certified) or 'jacobi'
     svt_warm: bool = True         # warm-start the Jacobi eigensolver from the previous iteration
     svt_gram_first: bool = False  # hold the sparse coding until the SVT Gram is done (always for Jacobi)
@@ -61,7 +61,8 @@ class LrsPnPConfig:
         return LrsPnPConfig(**base)
 
 
-_ALPHA = {"spec2": ops.ALPHA_SPEC2, "fro4": ops.ALPHA_FRO4, "soft": ops.ALPHA_SOFT}
+_ALPHA = {"spec2": ops.ALPHA_SPEC2, "fro4": ops.ALPHA_FRO4, "soft": ops.ALPHA_SOFT, "matlab": ops.ALPHA_SPEC2}
+_PROX = {"spec2": ops.PROX_NLM, "fro4": ops.PROX_NLM, "soft": ops.PROX_SOFT, "matlab": ops.PROX_NLM_MATLAB}
 
 
 class LrsPnP:
@@ -87,7 +88,9 @@ class LrsPnP:
         self.gamma32, self.mu1_32, self.mu2_32 = f32(cfg.gamma), f32(cfg.mu1), f32(cfg.mu2)
         self.c2 = f32(1 / cfg.mu2)                        # (1/mu_2)*lambda_2   main_LRS_PnP.py:315
         self.tau = float(f32(1 / cfg.mu2))                # SVT threshold (float32 in numpy)
-        self.prox = ops.PROX_SOFT if cfg.variant == "soft" else ops.PROX_NLM
+        if cfg.variant not in _PROX:
+            raise LrsError(f"unknown ISTA variant {cfg.variant!r} (spec2 | fro4 | soft | matlab)")
+        self.prox = _PROX[cfg.variant]
 
         # ---- block grid (host bookkeeping) -------------------------------------------------
         rows, cols = ops.block_grid(self.P, self.B, cfg.bb, cfg.sliding)

@@ -24,8 +24,9 @@
 #include <string.h>
 
 void oracle_nlm_col(const float *g, long K, long ldg, double h, float *out, long ldo);
+void oracle_nlm_matlab_col(const float *g, long K, long ldg, double h, float *out, long ldo);
 
-enum { ORACLE_PROX_NLM = 0, ORACLE_PROX_SOFT = 1 };
+enum { ORACLE_PROX_NLM = 0, ORACLE_PROX_SOFT = 1, ORACLE_PROX_NLM_MATLAB = 2 };
 
 /*
  * One block of the sparse-coding prox.
@@ -33,7 +34,7 @@ enum { ORACLE_PROX_NLM = 0, ORACLE_PROX_SOFT = 1 };
  *   obs   [n]    1 where the observed block (blocks_copy, :244) is non-zero, 0 where pruned (:278)
  *   D     [n*K]  Full_Dictionary, row-major (D[r*K + k])
  *   alpha        ISTA step normaliser (float32, as numpy returns it)
- *   thr          NLM h (prox NLM) or soft threshold T (prox SOFT)
+ *   thr          NLM h (prox NLM, NLM_MATLAB) or soft threshold T (prox SOFT)
  *   x     [K]    out: Coefs
  *   phi   [n]    out: Full_Dictionary @ Coefs (may be NULL)
  */
@@ -69,6 +70,9 @@ void oracle_ista_block(const float *y, const uint8_t *obs, const float *D, long 
                 t = t > 0.0f ? t : 0.0f;
                 x[k] = g[k] > 0.0f ? t : (g[k] < 0.0f ? -t : 0.0f);
             }
+        } else if (prox == ORACLE_PROX_NLM_MATLAB) {
+            /* pnp_ista.m:30 NLmeansfilter(gradient, 3, 3, 0.1*T); thr = 0.1*T */
+            oracle_nlm_matlab_col(g, K, 1, thr, x, 1);
         } else {
             oracle_nlm_col(g, K, 1, thr, x, 1);
         }

@@ -168,3 +168,58 @@ void oracle_nlm_col(const float *g, long K, long ldg, double h, float *out, long
     }
     free(v);
 }
+
+/*
+ * The MATLAB variant of the PnP prox (LRS-PnP(Matlab Code)/pnp_ista.m:30 calls
+ * NLmeansfilter(gradient, 3, 3, 0.1*T)), restated for a (K,1) column in fp64
+ * (NLmeansfilter.m:18-78):
+ *   input2 = padarray(g, [3 3], 'symmetric')  -> g-hat[j] = g[-j-1] (j < 0), g[2K-1-j] (j >= K);
+ *   kernel = make_kernel(3) normalised (sum 1); for a one-column image every column of the 7x7
+ *   windows is the same, so d = sum_u krow[u] (g-hat[i+u] - g-hat[r+u])^2 with krow[u] the row
+ *   sums of the kernel, (1/3) sum_{d=max(|u|,1)..3} 1/(2d+1);
+ *   w = exp(-d / h^2) over r in [i-3, i+3] clipped to [0, K-1], r != i; wmax = max w;
+ *   out = (sum w g[r] + wmax g[i]) / (sum w + wmax), or g[i] when that sum is 0.
+ * Evaluation order (shared bit for bit with the HIP kernel, -ffp-contract=off): d accumulated over
+ * u = -3..3 as d + krow*(diff*diff); neighbours r ascending.  MATLAB's own order of the 7x7 sum
+ * (columns first) is not reproduced: there is no MATLAB/Octave here, so this mode is pinned by
+ * a literal transcription of NLmeansfilter.m (oracle.py: nlm_matlab_literal), not by MATLAB.
+ */
+void oracle_nlm_matlab_krow(double krow[7]) {
+    for (int u = -3; u <= 3; ++u) {
+        const int a = u < 0 ? -u : u;
+        double s = 0.0;
+        for (int d = (a < 1 ? 1 : a); d <= 3; ++d) s = s + 1.0 / (double)(2 * d + 1);
+        krow[u + 3] = s / 3.0;
+    }
+}
+
+void oracle_nlm_matlab_col(const float *g, long K, long ldg, double h, float *out, long ldo) {
+    double krow[7];
+    oracle_nlm_matlab_krow(krow);
+    const double h2 = h * h;
+    double *v = (double *)malloc(sizeof(double) * (size_t)(K + 6));
+    for (long j = -3; j < K + 3; ++j) {
+        const long s = j < 0 ? -j - 1 : (j >= K ? 2 * K - 1 - j : j);
+        v[j + 3] = (double)g[s * ldg];
+    }
+    for (long i = 0; i < K; ++i) {
+        double sw = 0.0, av = 0.0, wmax = 0.0;
+        for (int t = -3; t <= 3; ++t) {
+            const long r = i + t;
+            if (t == 0 || r < 0 || r >= K) continue;
+            double d = 0.0;
+            for (int u = -3; u <= 3; ++u) {
+                const double df = v[i + u + 3] - v[r + u + 3];
+                d = d + krow[u + 3] * (df * df);
+            }
+            const double w = exp(-d / h2);
+            if (w > wmax) wmax = w;
+            sw = sw + w;
+            av = av + w * v[r + 3];
+        }
+        av = av + wmax * v[i + 3];
+        sw = sw + wmax;
+        out[i * ldo] = sw > 0.0 ? (float)(av / sw) : g[i * ldg];
+    }
+    free(v);
+}

@@ -52,6 +52,8 @@ def lib():
         L.oracle_nlm_fast2d.argtypes = [f32, c_int, c_int, c_int, c_int, c_int, c_double, c_double, f32]
         L.oracle_nlm_col.restype = None
         L.oracle_nlm_col.argtypes = [f32, c_long, c_long, c_double, f32, c_long]
+        L.oracle_nlm_matlab_col.restype = None
+        L.oracle_nlm_matlab_col.argtypes = [f32, c_long, c_long, c_double, f32, c_long]
         L.oracle_ista_block.restype = None
         L.oracle_ista_block.argtypes = [f32, u8, f32, c_long, c_long, c_float, c_double, c_int, c_int,
                                         f32, ctypes.c_void_p]
@@ -68,7 +70,7 @@ def lib():
     return _lib
 
 
-PROX_NLM, PROX_SOFT = 0, 1
+PROX_NLM, PROX_SOFT, PROX_NLM_MATLAB = 0, 1, 2
 
 
 # --------------------------------------------------------------------------------------------
@@ -93,6 +95,53 @@ def nlm_col(g: np.ndarray, h: float) -> np.ndarray:
     g = np.ascontiguousarray(g, dtype=np.float32).reshape(-1)
     out = np.empty_like(g)
     lib().oracle_nlm_col(g, g.size, 1, float(h), out, 1)
+    return out
+
+
+def nlm_matlab_col(g: np.ndarray, h: float) -> np.ndarray:
+    """NLmeansfilter(g, 3, 3, h) for a (K,1) column, closed form in C (nlm_oracle.c)."""
+    g = np.ascontiguousarray(g, dtype=np.float32).reshape(-1)
+    out = np.empty_like(g)
+    lib().oracle_nlm_matlab_col(g, g.size, 1, float(h), out, 1)
+    return out
+
+
+def nlm_matlab_literal(image: np.ndarray, t: int, f: int, h: float) -> np.ndarray:
+    """Literal transcription of LRS-PnP(Matlab Code)/NLmeansfilter.m:1-91 (any m x n image,
+    fp64, MATLAB's 1-based loops shifted by one, padarray 'symmetric', make_kernel, the
+    sum(sum(.)) of column sums).  Slow: the pin of nlm_matlab_col on small inputs."""
+    inp = np.asarray(image, dtype=np.float64)
+    m, n = inp.shape
+    input2 = np.pad(inp, f, mode="symmetric")                      # padarray(input,[f f],'symmetric')
+    kernel = np.zeros((2 * f + 1, 2 * f + 1))                     # make_kernel(f)  :80-91
+    for d in range(1, f + 1):
+        value = 1.0 / (2 * d + 1) ** 2
+        for i in range(-d, d + 1):
+            for j in range(-d, d + 1):
+                kernel[f - i, f - j] = kernel[f - i, f - j] + value
+    kernel = kernel / f
+    kernel = kernel / kernel.sum(axis=0).sum()                    # kernel / sum(sum(kernel))
+    h = h * h
+    out = np.zeros((m, n))
+    for i in range(1, m + 1):
+        for j in range(1, n + 1):
+            i1, j1 = i + f, j + f
+            W1 = input2[i1 - f - 1:i1 + f, j1 - f - 1:j1 + f]
+            wmax = average = sweight = 0.0
+            for r in range(max(i1 - t, f + 1), min(i1 + t, m + f) + 1):
+                for s_ in range(max(j1 - t, f + 1), min(j1 + t, n + f) + 1):
+                    if r == i1 and s_ == j1:
+                        continue
+                    W2 = input2[r - f - 1:r + f, s_ - f - 1:s_ + f]
+                    d = (kernel * (W1 - W2) * (W1 - W2)).sum(axis=0).sum()
+                    w = np.exp(-d / h)
+                    if w > wmax:
+                        wmax = w
+                    sweight = sweight + w
+                    average = average + w * input2[r - 1, s_ - 1]
+            average = average + wmax * input2[i1 - 1, j1 - 1]
+            sweight = sweight + wmax
+            out[i - 1, j - 1] = average / sweight if sweight > 0 else inp[i - 1, j - 1]
     return out
 
 
@@ -135,12 +184,13 @@ def ista_alpha_h(H: np.ndarray, lambda_ista: float, variant: str):
     variant 'spec2' : main_LRS_PnP.py:134-146     alpha = ||H||_2^2, NLM h = 0.1*T
     variant 'fro4'  : …1-LiP.py:187-196            alpha = 2(tr(H^T H)+tr(H^T H)), h = T
     variant 'soft'  : ista.m:15-23                 alpha = ||H||_2^2, soft threshold T
+    variant 'matlab': pnp_ista.m:16,30             alpha = max eig(H^T H), NLmeansfilter h = 0.1*T
     """
     H = np.asarray(H, dtype=np.float32)
     if H.shape[0] == 0:
         # no observed row: the reference divides by alpha = 0 (undefined); lrspnp's convention
         return np.float32(1.0), 1.0
-    if variant in ("spec2", "soft"):
+    if variant in ("spec2", "soft", "matlab"):
         alpha = np.linalg.norm(H, 2) ** 2
     elif variant == "fro4":
         G = H.T @ H
@@ -149,7 +199,7 @@ def ista_alpha_h(H: np.ndarray, lambda_ista: float, variant: str):
         raise ValueError(variant)
     alpha = np.float32(alpha)
     T = np.float32(lambda_ista) / (np.float32(2) * alpha)
-    if variant == "spec2":
+    if variant in ("spec2", "matlab"):      # pnp_ista.m:30 NLmeansfilter(., 3, 3, T*0.1)
         thr = T * np.float32(0.1)
     else:
         thr = T
@@ -222,7 +272,7 @@ class LrsPnpOracle:
         self.bb, self.sliding = bb, sliding
         self.gamma, self.mu1, self.mu2 = gamma, mu1, mu2
         self.Nit, self.variant = Nit, variant
-        self.prox = PROX_SOFT if variant == "soft" else PROX_NLM
+        self.prox = {"soft": PROX_SOFT, "matlab": PROX_NLM_MATLAB}.get(variant, PROX_NLM)
         self.rows, self.cols = block_grid(self.P, self.B, bb, sliding)
         self.nb = self.rows.size
         blocks_copy = im2col(self.Y, bb, self.rows, self.cols)       # :244

@@ -84,7 +84,8 @@ def _rand_blocks(rng, nb, n, miss_frac, scale=0.3):
 
 @pytest.mark.parametrize("bb,nb,Nit,variant", [(8, 300, 80, "spec2"), (8, 129, 100, "fro4"),
                                                (8, 64, 40, "soft"), (36, 20, 12, "fro4"),
-                                               (36, 9, 10, "spec2")])
+                                               (36, 9, 10, "spec2"), (8, 70, 30, "matlab"),
+                                               (36, 5, 8, "matlab")])
 def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant):
     from lrspnp.data import synthetic_dictionary
     rng = np.random.default_rng(bb * 1000 + nb)
@@ -95,7 +96,7 @@ def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant):
     alpha = np.empty(nb, np.float32); thr = np.empty(nb, np.float64)
     for j in range(nb):
         alpha[j], thr[j] = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, variant)
-    prox = O.PROX_SOFT if variant == "soft" else O.PROX_NLM
+    prox = {"soft": O.PROX_SOFT, "matlab": O.PROX_NLM_MATLAB}.get(variant, O.PROX_NLM)
     Xo, PHIo = O.ista_batch(Yb, obs, D, alpha, thr, Nit, prox)
     pad = lambda a: np.pad(a, ((0, 0), (0, n_pad - n)))
     d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
@@ -104,8 +105,13 @@ def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant):
     coefs = coefs.cpu().numpy()
     worst = max(rel(coefs[j], Xo[j]) for j in range(nb))
     worst_phi = max(rel(phi[j], PHIo[j]) for j in range(nb))
-    assert worst < 1e-5, worst
-    assert worst_phi < 1e-5, worst_phi
+    # The MATLAB variant's exp(-d/h^2) weights (no cutoff) amplify the ~1-ulp float32 difference
+    # between the MFMA and the oracle's products: d/h^2 ~ 1e2-1e3 at the reference's h, so the
+    # weights move by ~2 diff dg / h^2 ~ 1e-4 per iteration.  The prox itself is bit-exact
+    # (test_nlm_matlab_prox_bitexact); the iterated coefficients agree to 2e-2 here.
+    tol = 2e-2 if variant == "matlab" else 1e-5
+    assert worst < tol, worst
+    assert worst_phi < tol, worst_phi
 
 
 def test_ista_kernel_vs_reference_golden(ops, golden):
@@ -283,3 +289,47 @@ def test_ista_both_product_precisions_match_oracle():
     finally:
         L.lrs_ista_set_precision(1)
     assert rel(out[1][0], out[0][0]) < 1e-6
+
+
+def test_nlm_matlab_prox_bitexact():
+    """The in-register MATLAB-variant prox (NLmeansfilter.m closed form, fp64) against the oracle's
+    C restatement at several h (including h where the exp weights are tiny): same evaluation order,
+    so the only difference is exp() itself (device libm vs glibc, <= 1 fp64 ulp), which flips the
+    float32 rounding of an output in ~1e-4 of the elements: <= 1 float32 ulp."""
+    import ctypes
+    from lrspnp import _lib
+    f = _lib.device_lib().lrs_diag_nlm_matlab
+    vp = ctypes.c_void_p
+    f.argtypes = [vp, vp, ctypes.c_int64, vp, vp]
+    rng = np.random.default_rng(7)
+    nb = 40
+    g = (rng.standard_normal((nb, 256)) * 0.1).astype(np.float32)
+    h = np.geomspace(1e-4, 1.0, nb)
+    gd, hd = torch.from_numpy(g).cuda(), torch.from_numpy(h).cuda()
+    out = torch.empty_like(gd)
+    assert f(vp(gd.data_ptr()), vp(hd.data_ptr()), nb, vp(out.data_ptr()),
+             vp(torch.cuda.current_stream().cuda_stream)) == 0
+    ref = np.stack([O.nlm_matlab_col(g[j], h[j]) for j in range(nb)])
+    o = out.cpu().numpy()
+    np.testing.assert_array_max_ulp(o, ref, maxulp=1)
+    assert np.count_nonzero(o != ref) <= 1e-3 * o.size
+
+
+def test_compat_pnp_ista_vs_oracle(compat_mod=None):
+    """pnp_ista.m drop-in (compat.pnp_ista): NLmeansfilter prox, alpha = max eig(H^T H), h = 0.1 T;
+    against the oracle's C restatement, itself pinned to a literal transcription of NLmeansfilter.m
+    (tests/test_oracle.py::test_nlm_matlab_closed_form_vs_literal).  Parity vs MATLAB unpinned."""
+    from lrspnp import compat
+    from lrspnp.data import synthetic_dictionary
+    rng = np.random.default_rng(5)
+    D = synthetic_dictionary(64, 256, seed=1)
+    keep = rng.random(64) > 0.1
+    H = D[keep]
+    y = (0.3 * rng.standard_normal(H.shape[0])).astype(np.float32)
+    x = compat.pnp_ista(torch.from_numpy(y).view(-1, 1), torch.from_numpy(H), 0.1, None, 25).numpy().reshape(-1)
+    a, t = O.ista_alpha_h(H, 0.1, "matlab")
+    obs = keep.astype(np.uint8)
+    yb = np.zeros(64, np.float32)
+    yb[keep] = y
+    xo = O.ista_block(yb, obs, D, a, t, 25, O.PROX_NLM_MATLAB)[0]
+    assert rel(x, xo) < 2e-2      # see test_ista_kernel_vs_oracle: float32 rounding amplified by exp

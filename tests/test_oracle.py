@@ -94,3 +94,17 @@ def test_lrs_pnp_two_iterations_vs_reference(golden):
     assert rel(o.X, g["it2_X"]) < 1e-6
     p2 = O.psnr_bands(o.X, d["clean_img5"][0]).mean()
     assert round(p1, 2) == round(float(g["mpsnr"][0]), 2) and round(p2, 2) == round(float(g["mpsnr"][1]), 2)
+
+
+def test_nlm_matlab_closed_form_vs_literal():
+    """The MATLAB-variant prox (pnp_ista.m:30 -> NLmeansfilter.m): the oracle's C closed form for a
+    (K,1) column against a literal, loop-for-loop transcription of NLmeansfilter.m (padarray
+    'symmetric', make_kernel, sum(sum(.))).  No MATLAB/Octave here: this pins the restatement to
+    the reference file's own algorithm, not to MATLAB's arithmetic."""
+    rng = np.random.default_rng(0)
+    for K, h in [(16, 0.05), (40, 0.01), (64, 0.2), (9, 1.0), (256, 0.02)]:
+        g = (rng.standard_normal(K) * 0.1).astype(np.float32)
+        closed = O.nlm_matlab_col(g, h)
+        literal = O.nlm_matlab_literal(g.reshape(-1, 1).astype(np.float64), 3, 3, h).reshape(-1)
+        np.testing.assert_allclose(closed, literal.astype(np.float32), rtol=2e-7, atol=1e-9)
+        assert np.abs(closed - g).max() > 0      # the filter is not the identity at these h
