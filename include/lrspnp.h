@@ -273,6 +273,12 @@ int lrs_dipnet_last_loss(lrs_dipnet *net, double *loss, void *stream);
  * (pytorch_ssim/__init__.py:17-37; called at main_LRS_PnP_DIP_1-LiP.py:480-481); MSSIM =
  * acc / (C*H*W).  Images are [C][H][W] float32. */
 int lrs_ssim_f32(const float *img1, const float *img2, int C, int H, int W, double *acc, void *stream);
+/* Per-band PSNR 10 log10(255 / sqrt(mse_b)) (100 when mse_b < 1e-10) of X against C, both P x B
+ * float32 unfolded (main_LRS_PnP.py:379-384, psnr() :40-46, bach_mpsnr :49-58); psnr: device, B
+ * doubles.  fp64 accumulation, fixed-order reduction (deterministic). */
+size_t lrs_psnr_workspace(int64_t P, int64_t B);
+int lrs_psnr_bands_f32(const float *X, const float *C, int64_t P, int64_t B, double *psnr, void *ws,
+                       size_t ws_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -52,7 +52,61 @@ __global__ __launch_bounds__(256) void k_ssim(const float *__restrict__ a, const
 
 }  // namespace lrs
 
+namespace lrs {
+
+// ---- per-band PSNR on the unfolded matrices (main_LRS_PnP.py:379-384; psnr() :40-46) --------
+// Stage 1: workgroup s sums (X - C)^2 over its slab of rows for every band (threads over bands,
+// coalesced rows, fp64); stage 2: one thread per band reduces the slabs in fixed order and
+// applies the reference's 10 log10(255 / sqrt(mse)) (100 when mse < 1e-10, as psnr() does).
+constexpr int kPsnrSlabs = 256;
+
+__global__ __launch_bounds__(256) void k_psnr_partial(const float *__restrict__ X, const float *__restrict__ C,
+                                                      int64_t P, int B, int64_t rows, double *__restrict__ part) {
+    const int64_t r0 = (int64_t)blockIdx.x * rows, r1 = min<int64_t>(P, r0 + rows);
+    for (int b = threadIdx.x; b < B; b += 256) {
+        double s = 0.0;
+        for (int64_t r = r0; r < r1; ++r) {
+            const double d = (double)X[r * B + b] - (double)C[r * B + b];
+            s = __fma_rn(d, d, s);
+        }
+        part[(int64_t)blockIdx.x * B + b] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_psnr_finish(const double *__restrict__ part, int nslab, int64_t P, int B,
+                                                     double *__restrict__ psnr) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    double s = 0.0;
+    for (int k = 0; k < nslab; ++k) s += part[(int64_t)k * B + b];
+    const double mse = s / (double)P;
+    psnr[b] = mse < 1.0e-10 ? 100.0 : 10.0 * log10(255.0 / sqrt(mse));
+}
+
+}  // namespace lrs
+
 using namespace lrs;
+
+extern "C" size_t lrs_psnr_workspace(int64_t P, int64_t B) {
+    if (P <= 0 || B <= 0) return 0;
+    return (size_t)kPsnrSlabs * (size_t)B * sizeof(double);
+}
+
+// psnr (device, B doubles) <- per-band PSNR of X against C, both P x B float32 (unfolded).
+extern "C" int lrs_psnr_bands_f32(const float *X, const float *C, int64_t P, int64_t B, double *psnr, void *ws,
+                                  size_t ws_bytes, void *stream) {
+    if (!X || !C || !psnr || !ws || P <= 0 || B <= 0) return LRS_E_INVALID;
+    if (ws_bytes < lrs_psnr_workspace(P, B)) return LRS_E_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t rows = (P + kPsnrSlabs - 1) / kPsnrSlabs;
+    const int nslab = (int)((P + rows - 1) / rows);
+    hipLaunchKernelGGL(k_psnr_partial, dim3((unsigned)nslab), dim3(256), 0, st, X, C, P, (int)B, rows, (double *)ws);
+    LRS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_psnr_finish, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, (const double *)ws, nslab, P,
+                       (int)B, psnr);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
 
 // acc (device double, zeroed by the call) receives sum of the SSIM map; mssim = acc / (C*H*W).
 extern "C" int lrs_ssim_f32(const float *img1, const float *img2, int C, int H, int W, double *acc, void *stream) {

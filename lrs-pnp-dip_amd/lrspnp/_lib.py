@@ -53,6 +53,8 @@ def _declare(L):
         "lrs_ista_alpha_f32": (i32, [vp, i64, i64, vp, i64, i64, i32, f32, vp, vp, vp, sz, vp]),
         "lrs_ista_f32": (i32, [vp, vp, vp, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp, vp]),
         "lrs_ssim_f32": (i32, [vp, vp, i32, i32, i32, vp, vp]),
+        "lrs_psnr_workspace": (sz, [i64, i64]),
+        "lrs_psnr_bands_f32": (i32, [vp, vp, i64, i64, vp, vp, sz, vp]),
         "lrs_ista_set_precision": (i32, [i32]),
         "lrs_ista_get_precision": (i32, []),
         "lrs_svt_workspace": (sz, [i64, i64]),

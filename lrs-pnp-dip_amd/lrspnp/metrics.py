@@ -1,6 +1,7 @@
-"""Quality metrics of the reference (not timed): per-band PSNR with its 10*log10(255/RMSE)
-definition and the band mean (main_LRS_PnP.py:40-58, :379-384), and MSSIM (pytorch_ssim.ssim,
-main_LRS_PnP_DIP_1-LiP.py:480-481) on the HIP kernel lrs_ssim_f32."""
+"""Quality metrics of the reference (not timed), on the device: per-band PSNR with its
+10*log10(255/RMSE) definition and the band mean (main_LRS_PnP.py:40-58, :379-384) on the HIP kernel
+lrs_psnr_bands_f32, and MSSIM (pytorch_ssim.ssim, main_LRS_PnP_DIP_1-LiP.py:480-481) on lrs_ssim_f32.
+Nothing leaves the GPU but the final scalar."""
 from __future__ import annotations
 
 import torch
@@ -13,10 +14,22 @@ def fold(X: torch.Tensor, H: int, W: int) -> torch.Tensor:
 
 
 def psnr_bands(X: torch.Tensor, clean_bhw: torch.Tensor) -> torch.Tensor:
+    """Per-band PSNR (device float64 [B]) of the unfolded X (P x B) against clean (B, H, W)."""
+    import ctypes
+
+    from . import ops
+    from ._lib import check, device_lib
     B, H, W = clean_bhw.shape
-    img = fold(X, H, W).double()
-    mse = ((img - clean_bhw.double()) ** 2).mean(dim=(1, 2))
-    return 10.0 * torch.log10(255.0 / torch.sqrt(mse))
+    C = ops.image_to_unfolded(clean_bhw.contiguous().float(), H, W)
+    Xc = X.contiguous().float()
+    L = device_lib()
+    P = H * W
+    ws = torch.empty(int(L.lrs_psnr_workspace(P, B)), dtype=torch.uint8, device=X.device)
+    out = torch.empty(B, dtype=torch.float64, device=X.device)
+    vp = ctypes.c_void_p
+    check(L.lrs_psnr_bands_f32(vp(Xc.data_ptr()), vp(C.data_ptr()), P, B, vp(out.data_ptr()), vp(ws.data_ptr()),
+                               ws.numel(), vp(torch.cuda.current_stream().cuda_stream)), "lrs_psnr_bands_f32")
+    return out
 
 
 def mpsnr(X: torch.Tensor, clean_bhw: torch.Tensor) -> float:

@@ -333,3 +333,20 @@ def test_compat_pnp_ista_vs_oracle(compat_mod=None):
     yb[keep] = y
     xo = O.ista_block(yb, obs, D, a, t, 25, O.PROX_NLM_MATLAB)[0]
     assert rel(x, xo) < 2e-2      # see test_ista_kernel_vs_oracle: float32 rounding amplified by exp
+
+
+def test_psnr_bands_kernel_vs_oracle():
+    """lrs_psnr_bands_f32 (metrics.psnr_bands / mpsnr) vs the oracle's per-band PSNR
+    (main_LRS_PnP.py:379-384), including a band equal to the reference (psnr() returns 100)."""
+    from lrspnp.metrics import psnr_bands
+    rng = np.random.default_rng(3)
+    B, H, W = 37, 29, 31
+    clean = rng.random((B, H, W)).astype(np.float32)
+    noisy = (clean + 0.05 * rng.standard_normal((B, H, W))).astype(np.float32)
+    noisy[5] = clean[5]
+    X = np.ascontiguousarray(noisy.transpose(2, 1, 0).reshape(H * W, B))    # unfold: p = i + H j
+    got = psnr_bands(torch.from_numpy(X).cuda(), torch.from_numpy(clean).cuda()).cpu().numpy()
+    ref = O.psnr_bands(X, clean)
+    assert got[5] == 100.0
+    mask = np.arange(B) != 5
+    np.testing.assert_allclose(got[mask], ref[mask], rtol=1e-6)
