@@ -102,6 +102,14 @@ int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n,
 int lrs_ista_set_precision(int precision);
 int lrs_ista_get_precision(void);
 
+/* Arithmetic of the DIP engine's large conv GEMMs (128x128 tiles), process-wide:
+ * LRS_DIP_SPLIT_BF16 (default): bf16 matrix cores on operands split into three bf16 terms, six
+ * partial products, fp32 accumulation (fp32-GEMM accuracy); LRS_DIP_F32: v_mfma_f32_16x16x4_f32. */
+#define LRS_DIP_F32 0
+#define LRS_DIP_SPLIT_BF16 1
+int lrs_dip_set_precision(int precision);
+int lrs_dip_get_precision(void);
+
 /* ---- SVT low-rank prox ---------------------------------------------------------------------
  * U = SVT(Z, tau) with Z = X + c2 * L2 (c2 = float(1/mu_2); L2 may be NULL), via an fp64 Gram
  * Z^T Z, a one-workgroup symmetric eigensolver and U = Z * V diag(max(1 - tau/s, 0)) V^T.

@@ -158,6 +158,141 @@ __global__ __launch_bounds__(kGemmThreads) void k_gemm(GemmArgs g) {
         }
 }
 
+// ---- split-bf16 variant of the 128x128 GEMM (BK 32) ---------------------------------------------
+// Same tiling and pipeline as k_gemm, but the products run on v_mfma_f32_16x16x32_bf16: every fp32
+// operand is split exactly into three bf16 terms (hi + mid + lo) when its fragment leaves LDS and
+// the six partial products with i + j <= 4 are accumulated in fp32 (the dropped ones are <= 2^-24
+// relative: fp32-GEMM accuracy, the ISTA kernel's scheme).  2.7x fewer matrix-core cycles than the
+// f32 MFMA for the same tile.
+constexpr int kBK32 = 32, kLdsK32 = kBK32 + 4;
+typedef __bf16 gbf16x8 __attribute__((ext_vector_type(8)));
+
+template <bool KCONTIG>
+__device__ __forceinline__ void load_tile32(const float *__restrict__ S, int ld, int k0, int kend, int x0, int X,
+                                            float4 (&r)[4]) {
+    const int t = threadIdx.x;
+    float v[16];
+    if (KCONTIG) {
+        const int x = x0 + (t >> 1), kb = k0 + 16 * (t & 1);
+        const float *src = S + (int64_t)x * ld;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = (x < X && kb + u < kend) ? src[kb + u] : 0.0f;
+    } else {
+        const int x = x0 + (t & 127), kb = k0 + 16 * (t >> 7);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = (x < X && kb + u < kend) ? S[(int64_t)(kb + u) * ld + x] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = float4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+}
+
+__device__ __forceinline__ void store_tile32(float (*T)[kLdsK32], const float4 (&r)[4], bool kcontig) {
+    const int t = threadIdx.x;
+    const int x = kcontig ? (t >> 1) : (t & 127);
+    const int kb = kcontig ? 16 * (t & 1) : 16 * (t >> 7);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<float4 *>(&T[x][kb + 4 * q]) = r[q];
+}
+
+__device__ __forceinline__ void gsplit8(const float4 &a, const float4 &b, gbf16x8 (&f)[3]) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const __bf16 h = (__bf16)v[e];
+        const float r1 = v[e] - (float)h;
+        const __bf16 m = (__bf16)r1;
+        f[0][e] = h;
+        f[1][e] = m;
+        f[2][e] = (__bf16)(r1 - (float)m);
+    }
+}
+
+__device__ __forceinline__ floatx4 gmfma6(const gbf16x8 (&A)[3], const gbf16x8 (&B)[3], floatx4 acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[2], B[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[0], acc, 0, 0, 0);
+    return acc;
+}
+
+template <int TA, int TB>
+__global__ __launch_bounds__(kGemmThreads) void k_gemm_b3(GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) float As[2][kBM][kLdsK32];
+    __shared__ __attribute__((aligned(16))) float Bs[2][kBN][kLdsK32];
+    const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+    const int kbeg = blockIdx.z * g.kchunk;
+    const int kend = min(g.K, kbeg + g.kchunk);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
+    const int jl = lane & 15, gk = lane >> 4;
+    const int lda = TA ? g.M : g.K;
+    const int ldb = TB ? g.K : g.N;
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float4 ra[4], rb[4];
+    load_tile32<TA == 0>(g.A, lda, kbeg, kend, m0, g.M, ra);
+    load_tile32<TB == 1>(g.B, ldb, kbeg, kend, n0, g.N, rb);
+    int stage = 0;
+    store_tile32(As[0], ra, TA == 0);
+    store_tile32(Bs[0], rb, TB == 1);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += kBK32) {
+        const bool more = k0 + kBK32 < kend;
+        if (more) {
+            load_tile32<TA == 0>(g.A, lda, k0 + kBK32, kend, m0, g.M, ra);
+            load_tile32<TB == 1>(g.B, ldb, k0 + kBK32, kend, n0, g.N, rb);
+        }
+        // fragments: 8 consecutive k (8 gk .. 8 gk + 7) of row / column 16 a + jl
+        gbf16x8 fb[4][3];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const float *src = &Bs[stage][wn + 16 * b + jl][8 * gk];
+            gsplit8(*reinterpret_cast<const float4 *>(src), *reinterpret_cast<const float4 *>(src + 4), fb[b]);
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            gbf16x8 fa[3];
+            const float *src = &As[stage][wm + 16 * a + jl][8 * gk];
+            gsplit8(*reinterpret_cast<const float4 *>(src), *reinterpret_cast<const float4 *>(src + 4), fa);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) acc[a][b] = gmfma6(fa, fb[b], acc[a][b]);
+        }
+        if (more) {
+            store_tile32(As[stage ^ 1], ra, TA == 0);   // the other stage: last read one step ago
+            store_tile32(Bs[stage ^ 1], rb, TB == 1);
+        }
+        __syncthreads();
+        stage ^= 1;
+    }
+    float *C = g.C + (int64_t)blockIdx.z * g.M * g.N;
+    const bool final_out = gridDim.z == 1;
+    const float dv = (final_out && g.div) ? *g.div : 1.0f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int n = n0 + wn + 16 * b + jl;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm + 16 * a + 4 * gk + r;
+                if (m < g.M && n < g.N) {
+                    float v = acc[a][b][r];
+                    if (final_out) {
+                        if (g.bias) v = v + g.bias[m];
+                        if (g.div) v = v / dv;
+                        if (g.accum) v = C[(int64_t)m * g.N + n] + v;
+                    }
+                    C[(int64_t)m * g.N + n] = v;
+                }
+            }
+        }
+}
+
 // ---- small-tile variant (64x64, BK 16, 2x2 waves of 32x32) for GEMMs whose 128-tile grid is
 // too small to fill the chip (the 36x36 native U-Net layers) ----------------------------------
 constexpr int kBM64 = 64, kBN64 = 64, kBK64 = 16;
@@ -297,15 +432,15 @@ __device__ __forceinline__ int reflect_idx(int u, int n) {   // ReflectionPad2d 
     return u;
 }
 
-__global__ void k_im2col(const float *__restrict__ x, ConvGeom gm, float *__restrict__ col) {
-    const int64_t P = (int64_t)gm.Ho * gm.Wo;
-    const int64_t total = (int64_t)gm.Cin * gm.k * gm.k * P;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = i / P;
-        const int p = (int)(i - r * P);
-        const int kx = (int)(r % gm.k), ky = (int)((r / gm.k) % gm.k), c = (int)(r / (gm.k * gm.k));
-        const int oy = p / gm.Wo, ox = p - oy * gm.Wo;
+// One col row r = (c, ky, kx) per blockIdx.y (grid-strided), the output pixels of that row across
+// blockIdx.x: 32-bit index arithmetic, c / ky / kx uniform per workgroup.
+__global__ __launch_bounds__(256) void k_im2col(const float *__restrict__ x, ConvGeom gm, float *__restrict__ col) {
+    const int P = gm.Ho * gm.Wo, kk = gm.k * gm.k, Kc = gm.Cin * kk;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const int oy = p / gm.Wo, ox = p - oy * gm.Wo;
+    for (int r = blockIdx.y; r < Kc; r += gridDim.y) {
+        const int c = r / kk, kyx = r - c * kk, ky = kyx / gm.k, kx = kyx - ky * gm.k;
         int uy = oy * gm.stride + ky - gm.pad, ux = ox * gm.stride + kx - gm.pad;
         float v = 0.0f;
         bool inside = true;
@@ -319,7 +454,7 @@ __global__ void k_im2col(const float *__restrict__ x, ConvGeom gm, float *__rest
             const int sy = gm.up ? (uy >> 1) : uy, sx = gm.up ? (ux >> 1) : ux;
             v = x[((int64_t)c * gm.Hs + sy) * gm.Ws + sx];
         }
-        col[i] = v;
+        col[(int64_t)r * P + p] = v;
     }
 }
 
@@ -336,41 +471,54 @@ __device__ __forceinline__ int padded_sources(int u, int n, int pad, int mode, i
     return cnt;
 }
 
-// dx[c][y][x] = sum over every col entry that read it (adjoint of k_im2col), gather form.
-__global__ void k_col2im(const float *__restrict__ dcol, ConvGeom gm, float *__restrict__ dx, int accum) {
-    const int64_t total = (int64_t)gm.Cin * gm.Hs * gm.Ws;
-    const int64_t P = (int64_t)gm.Ho * gm.Wo;
-    const int k = gm.k, s = gm.stride;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int sx = (int)(i % gm.Ws), sy = (int)((i / gm.Ws) % gm.Hs), c = (int)(i / ((int64_t)gm.Ws * gm.Hs));
-        float acc = 0.0f;
-        const int nup = gm.up ? 2 : 1;
-        for (int a = 0; a < nup; ++a) {
-            const int uy = gm.up ? 2 * sy + a : sy;
-            int iys[3];
-            const int ny = padded_sources(uy, gm.Hu, gm.pad, gm.pad_mode, iys);
-            for (int b = 0; b < nup; ++b) {
-                const int ux = gm.up ? 2 * sx + b : sx;
-                int ixs[3];
-                const int nx = padded_sources(ux, gm.Wu, gm.pad, gm.pad_mode, ixs);
-                for (int py = 0; py < ny; ++py)
-                    for (int ky = 0; ky < k; ++ky) {
-                        const int ty = iys[py] - ky;
-                        if (ty < 0 || ty % s) continue;
-                        const int oy = ty / s;
-                        if (oy >= gm.Ho) continue;
-                        for (int px = 0; px < nx; ++px)
-                            for (int kx = 0; kx < k; ++kx) {
-                                const int tx = ixs[px] - kx;
-                                if (tx < 0 || tx % s) continue;
-                                const int ox = tx / s;
-                                if (ox >= gm.Wo) continue;
-                                acc += dcol[((int64_t)(c * k + ky) * k + kx) * P + (int64_t)oy * gm.Wo + ox];
-                            }
-                    }
-            }
+// dx[c][y][x] = sum over every col entry that read it (adjoint of k_im2col), gather form.  One
+// channel per blockIdx.y (grid-strided), its pixels across blockIdx.x; 32-bit index arithmetic and
+// the stride as a template parameter (1 and 2 are the nets' strides).
+template <int STRIDE>
+__device__ __forceinline__ float col2im_pixel(const float *__restrict__ dcol, const ConvGeom &gm, int c, int sy,
+                                              int sx, int P) {
+    const int k = gm.k;
+    const int s = STRIDE > 0 ? STRIDE : gm.stride;
+    float acc = 0.0f;
+    const int nup = gm.up ? 2 : 1;
+    for (int a = 0; a < nup; ++a) {
+        const int uy = gm.up ? 2 * sy + a : sy;
+        int iys[3];
+        const int ny = padded_sources(uy, gm.Hu, gm.pad, gm.pad_mode, iys);
+        for (int b = 0; b < nup; ++b) {
+            const int ux = gm.up ? 2 * sx + b : sx;
+            int ixs[3];
+            const int nx = padded_sources(ux, gm.Wu, gm.pad, gm.pad_mode, ixs);
+            for (int py = 0; py < ny; ++py)
+                for (int ky = 0; ky < k; ++ky) {
+                    const int ty = iys[py] - ky;
+                    if (ty < 0 || ty % s) continue;
+                    const int oy = ty / s;
+                    if (oy >= gm.Ho) continue;
+                    for (int px = 0; px < nx; ++px)
+                        for (int kx = 0; kx < k; ++kx) {
+                            const int tx = ixs[px] - kx;
+                            if (tx < 0 || tx % s) continue;
+                            const int ox = tx / s;
+                            if (ox >= gm.Wo) continue;
+                            acc += dcol[(int64_t)((c * k + ky) * k + kx) * P + oy * gm.Wo + ox];
+                        }
+                }
         }
+    }
+    return acc;
+}
+
+template <int STRIDE>
+__global__ __launch_bounds__(256) void k_col2im(const float *__restrict__ dcol, ConvGeom gm, float *__restrict__ dx,
+                                                int accum) {
+    const int HW = gm.Hs * gm.Ws, P = gm.Ho * gm.Wo;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= HW) return;
+    const int sy = q / gm.Ws, sx = q - sy * gm.Ws;
+    for (int c = blockIdx.y; c < gm.Cin; c += gridDim.y) {
+        const float acc = col2im_pixel<STRIDE>(dcol, gm, c, sy, sx, P);
+        const int64_t i = (int64_t)c * HW + q;
         dx[i] = accum ? dx[i] + acc : acc;
     }
 }

@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -55,13 +56,19 @@ struct Split {
     bool big;   // 128x128 tiles (k_gemm) or 64x64 (k_gemm64)
 };
 
-// Tile choice and split-K: 128x128 tiles when they alone give >= 128 workgroups, else 64x64;
+// product arithmetic of the 128x128 conv GEMMs: LRS_DIP_SPLIT_BF16 (default) or LRS_DIP_F32
+static int g_dip_gemm_precision = LRS_DIP_SPLIT_BF16;
+
+// Tile choice and split-K: 128x128 tiles when they alone give >= 64 workgroups, else 64x64;
 // then split K until ~512 workgroups (2 per CU), keeping >= 128 of K per split and <= 64 splits.
-// (Measured: 128-tiles with deeper split-K on the small-N weight-gradient GEMMs, or a 1024-WG
-// target, are slower at both the 36x36 and the 196x196 sizes.)
-Split choose_split(int M, int N, int K) {
+// (Measured with the f32 kernels: 128-tiles with deeper split-K on the small-N weight-gradient
+// GEMMs, or a 1024-WG target, are slower at both the 36x36 and the 196x196 sizes.)
+Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision) {
     const int64_t t128 = (int64_t)((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
-    const bool big = t128 >= 128;
+    // long-K GEMMs (the weight gradients, K = pixels) take 128-tiles with deep split-K on the
+    // split-bf16 path when that still gives >= 256 workgroups (measured 25-30 % faster at 196^2 and
+    // 512^2; the 1x1 layer's 2-tile gradient is faster on 64-tiles)
+    const bool big = t128 >= 64 || (precision == LRS_DIP_SPLIT_BF16 && K >= 8192 && t128 >= 4);
     const int64_t tiles = big ? t128 : (int64_t)((M + kBM64 - 1) / kBM64) * ((N + kBN64 - 1) / kBN64);
     int S = 1;
     if (tiles < 256) {
@@ -71,16 +78,19 @@ Split choose_split(int M, int N, int K) {
         if (S > 64) S = 64;
         if (S < 1) S = 1;
     }
-    int kchunk = (int)round_up((K + S - 1) / S, kBK);
-    if (kchunk < kBK) kchunk = kBK;
+    const int bk = (big && precision == LRS_DIP_SPLIT_BF16) ? kBK32 : kBK;
+    int kchunk = (int)round_up((K + S - 1) / S, bk);
+    if (kchunk < bk) kchunk = bk;
     S = (K + kchunk - 1) / kchunk;
     if (S < 1) S = 1;
     return {S, kchunk, big};
 }
 
 int64_t gemm_part_floats(int M, int N, int K) {
-    const Split s = choose_split(M, N, K);
-    return s.S > 1 ? (int64_t)s.S * M * N : 0;
+    // sized for both precisions, so that the precision can change after a workspace was sized
+    const Split a = choose_split(M, N, K, LRS_DIP_F32), b = choose_split(M, N, K, LRS_DIP_SPLIT_BF16);
+    const int S = std::max(a.S, b.S);
+    return S > 1 ? (int64_t)S * M * N : 0;
 }
 
 // C = op(A) op(B) (+ bias) (/ *div); part: split-K scratch (>= gemm_part_floats)
@@ -93,7 +103,13 @@ int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
         g.C = part;
     }
-    if (s.big) {
+    if (s.big && g_dip_gemm_precision == LRS_DIP_SPLIT_BF16) {
+        dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, s.S);
+        if (!TA && !TB) hipLaunchKernelGGL((k_gemm_b3<0, 0>), grid, dim3(kGemmThreads), 0, st, g);
+        else if (!TA && TB) hipLaunchKernelGGL((k_gemm_b3<0, 1>), grid, dim3(kGemmThreads), 0, st, g);
+        else if (TA && !TB) hipLaunchKernelGGL((k_gemm_b3<1, 0>), grid, dim3(kGemmThreads), 0, st, g);
+        else hipLaunchKernelGGL((k_gemm_b3<1, 1>), grid, dim3(kGemmThreads), 0, st, g);
+    } else if (s.big) {
         dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, s.S);
         if (!TA && !TB) hipLaunchKernelGGL((k_gemm<0, 0>), grid, dim3(kGemmThreads), 0, st, g);
         else if (!TA && TB) hipLaunchKernelGGL((k_gemm<0, 1>), grid, dim3(kGemmThreads), 0, st, g);
@@ -131,8 +147,8 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
     const float *B = x;
     if (!plain_unit(g)) {
         if (!col) return LRS_E_WORKSPACE;
-        const int64_t n = (int64_t)Kc * P;
-        hipLaunchKernelGGL(k_im2col, dim3(ew_blocks(n, 1 << 16)), dim3(kEw), 0, st, x, g, col);
+        const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min(Kc, 65535));
+        hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, st, x, g, col);
         B = col;
     }
     return gemm(0, 0, w, B, y, bias, nullptr, Cout, P, Kc, part, part_cap, st);
@@ -148,8 +164,10 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
     if (!dcol) return LRS_E_WORKSPACE;
     rc = gemm(1, 0, w, gz, dcol, nullptr, nullptr, Kc, P, Cout, part, part_cap, st);
     if (rc) return rc;
-    const int64_t n = (int64_t)g.Cin * g.Hs * g.Ws;
-    hipLaunchKernelGGL(k_col2im, dim3(ew_blocks(n, 1 << 16)), dim3(kEw), 0, st, dcol, g, gx, accum_gx);
+    const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
+    if (g.stride == 1) hipLaunchKernelGGL(k_col2im<1>, grid, dim3(256), 0, st, dcol, g, gx, accum_gx);
+    else if (g.stride == 2) hipLaunchKernelGGL(k_col2im<2>, grid, dim3(256), 0, st, dcol, g, gx, accum_gx);
+    else hipLaunchKernelGGL(k_col2im<0>, grid, dim3(256), 0, st, dcol, g, gx, accum_gx);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -904,3 +922,11 @@ extern "C" int lrs_dipnet_last_loss(lrs_dipnet *net, double *loss, void *stream)
     *loss = acc / ((double)L.C * (double)L.P);
     return LRS_OK;
 }
+
+extern "C" int lrs_dip_set_precision(int precision) {
+    if (precision != LRS_DIP_F32 && precision != LRS_DIP_SPLIT_BF16) return LRS_E_INVALID;
+    g_dip_gemm_precision = precision;
+    return LRS_OK;
+}
+
+extern "C" int lrs_dip_get_precision(void) { return g_dip_gemm_precision; }

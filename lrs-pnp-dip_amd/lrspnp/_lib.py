@@ -57,6 +57,8 @@ def _declare(L):
         "lrs_psnr_bands_f32": (i32, [vp, vp, i64, i64, vp, vp, sz, vp]),
         "lrs_ista_set_precision": (i32, [i32]),
         "lrs_ista_get_precision": (i32, []),
+        "lrs_dip_set_precision": (i32, [i32]),
+        "lrs_dip_get_precision": (i32, []),
         "lrs_svt_workspace": (sz, [i64, i64]),
         "lrs_svt_f32": (i32, [vp, vp, f32, i64, i64, f64, vp, vp, i32, vp, sz, vp]),
         "lrs_svt_gram_f32": (i32, [vp, vp, f32, i64, i64, i32, vp, sz, vp]),

@@ -54,6 +54,8 @@ CONV_CASES = [
     (128, 198, 36, 36, 1, 1, 0, 1, 0),      # last 1x1 (plain)
     (7, 5, 11, 6, 3, 2, 1, 0, 0),           # zero padding, odd sizes
     (5, 9, 5, 7, 3, 1, 1, 1, 1),
+    (128, 128, 196, 196, 3, 1, 1, 1, 0),    # 196x196 layer: 128x128 GEMM tiles (split-bf16 path)
+    (64, 96, 100, 90, 3, 2, 1, 0, 0),       # 128-tiles with ragged M, N and K
 ]
 
 
@@ -66,8 +68,23 @@ def torch_conv(x, w, b, k, stride, pad, pad_mode, up):
     return F.conv2d(h, w, b, stride=stride)[0]
 
 
+@pytest.fixture(params=["split_bf16", "f32"])
+def precision(request, L):
+    # LRS_DIP_SPLIT_BF16 = 1 (default), LRS_DIP_F32 = 0: arithmetic of the 128x128 GEMM tiles
+    old = L.lrs_dip_get_precision()
+    assert L.lrs_dip_set_precision(1 if request.param == "split_bf16" else 0) == 0
+    yield request.param
+    L.lrs_dip_set_precision(old)
+
+
+def test_dip_precision_switch(L):
+    assert L.lrs_dip_get_precision() == 1          # split-bf16 by default
+    assert L.lrs_dip_set_precision(7) != 0
+    assert L.lrs_dip_get_precision() == 1
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_bwd(L, case):
+def test_conv_fwd_bwd(L, case, precision):
     cin, cout, H, W, k, stride, pad, pm, up = case
     g = torch.Generator().manual_seed(hash(case) & 0xffff)
     x = torch.randn(cin, H, W, generator=g)
