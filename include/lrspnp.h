@@ -172,7 +172,9 @@ int lrs_conv2d_out_size(int H, int W, int k, int stride, int pad, int upsample, 
 /* col workspace (floats) for lrs_conv2d_fwd_f32: Cin*k*k*Ho*Wo (0 when the unit is a plain 1x1). */
 int64_t lrs_conv2d_col_size(int Cin, int H, int W, int k, int stride, int pad, int upsample);
 /* y[Cout][Ho][Wo] = conv(pad(upsample(x))) + bias.  col receives the im2col matrix (kept for
- * the backward); ws/ws_bytes: split-K partials (lrs_conv2d_workspace). */
+ * the backward); col == NULL (k <= 3): implicit GEMM, the im2col is gathered inside the
+ * split-bf16 kernel and never stored (backward: lrs_conv2d_bwd_x_f32).
+ * ws/ws_bytes: split-K partials (lrs_conv2d_workspace). */
 size_t lrs_conv2d_workspace(int Cin, int H, int W, int Cout, int k, int stride, int pad, int upsample);
 int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const float *w, const float *bias,
                        int Cout, int k, int stride, int pad, int pad_mode, int upsample, float *col,
@@ -183,6 +185,10 @@ int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const float *w, co
 int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float *w, const float *w_div, int Cin,
                        int H, int W, int Cout, int k, int stride, int pad, int pad_mode, int upsample,
                        float *gx, float *gw, void *ws, size_t ws_bytes, void *stream);
+/* The same from the conv input x (k <= 3): gw's col^T is gathered inside the GEMM. */
+int lrs_conv2d_bwd_x_f32(const float *gy, const float *x, const float *w, const float *w_div, int Cin,
+                         int H, int W, int Cout, int k, int stride, int pad, int pad_mode, int upsample,
+                         float *gx, float *gw, void *ws, size_t ws_bytes, void *stream);
 
 /* y = act(BN_lip(z)) with batch statistics (gamma == NULL: y = act(z)).  Saves mean / invstd
  * [C]; running stats (nullable) get the momentum update.  ws: lrs_bn_act_workspace bytes,

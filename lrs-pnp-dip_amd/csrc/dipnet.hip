@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "dip_kernels.h"
+#include "dip_gemm.h"
 
 using namespace lrs;
 
@@ -63,12 +64,12 @@ static int g_dip_gemm_precision = LRS_DIP_SPLIT_BF16;
 // then split K until ~512 workgroups (2 per CU), keeping >= 128 of K per split and <= 64 splits.
 // (Measured with the f32 kernels: 128-tiles with deeper split-K on the small-N weight-gradient
 // GEMMs, or a 1024-WG target, are slower at both the 36x36 and the 196x196 sizes.)
-Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision) {
+Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision, bool force_big = false) {
     const int64_t t128 = (int64_t)((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
     // long-K GEMMs (the weight gradients, K = pixels) take 128-tiles with deep split-K on the
     // split-bf16 path when that still gives >= 256 workgroups (measured 25-30 % faster at 196^2 and
     // 512^2; the 1x1 layer's 2-tile gradient is faster on 64-tiles)
-    const bool big = t128 >= 64 || (precision == LRS_DIP_SPLIT_BF16 && K >= 8192 && t128 >= 4);
+    const bool big = force_big || t128 >= 64 || (precision == LRS_DIP_SPLIT_BF16 && K >= 8192 && t128 >= 4);
     const int64_t tiles = big ? t128 : (int64_t)((M + kBM64 - 1) / kBM64) * ((N + kBN64 - 1) / kBN64);
     int S = 1;
     if (tiles < 256) {
@@ -84,6 +85,12 @@ Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision) {
     S = (K + kchunk - 1) / kchunk;
     if (S < 1) S = 1;
     return {S, kchunk, big};
+}
+
+// split-K scratch of an implicit-GEMM conv product (always 128-tiles, split-bf16)
+int64_t s3_part_floats(int M, int N, int K) {
+    const Split s = choose_split(M, N, K, LRS_DIP_SPLIT_BF16, true);
+    return s.S > 1 ? (int64_t)s.S * M * N : 0;
 }
 
 int64_t gemm_part_floats(int M, int N, int K) {
@@ -105,10 +112,19 @@ int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *
     }
     if (s.big && g_dip_gemm_precision == LRS_DIP_SPLIT_BF16) {
         dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, s.S);
-        if (!TA && !TB) hipLaunchKernelGGL((k_gemm_b3<0, 0>), grid, dim3(kGemmThreads), 0, st, g);
-        else if (!TA && TB) hipLaunchKernelGGL((k_gemm_b3<0, 1>), grid, dim3(kGemmThreads), 0, st, g);
-        else if (TA && !TB) hipLaunchKernelGGL((k_gemm_b3<1, 0>), grid, dim3(kGemmThreads), 0, st, g);
-        else hipLaunchKernelGGL((k_gemm_b3<1, 1>), grid, dim3(kGemmThreads), 0, st, g);
+        const int lda = TA ? M : K, ldb = TB ? K : N;
+        if (!TA && !TB)
+            hipLaunchKernelGGL((k_gemm_s3<LdDense<true>, LdDense<false>>), grid, dim3(kGemmThreads), 0, st, g,
+                               LdDense<true>{A, lda, M}, LdDense<false>{B, ldb, N});
+        else if (!TA && TB)
+            hipLaunchKernelGGL((k_gemm_s3<LdDense<true>, LdDense<true>>), grid, dim3(kGemmThreads), 0, st, g,
+                               LdDense<true>{A, lda, M}, LdDense<true>{B, ldb, N});
+        else if (TA && !TB)
+            hipLaunchKernelGGL((k_gemm_s3<LdDense<false>, LdDense<false>>), grid, dim3(kGemmThreads), 0, st, g,
+                               LdDense<false>{A, lda, M}, LdDense<false>{B, ldb, N});
+        else
+            hipLaunchKernelGGL((k_gemm_s3<LdDense<false>, LdDense<true>>), grid, dim3(kGemmThreads), 0, st, g,
+                               LdDense<false>{A, lda, M}, LdDense<true>{B, ldb, N});
     } else if (s.big) {
         dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, s.S);
         if (!TA && !TB) hipLaunchKernelGGL((k_gemm<0, 0>), grid, dim3(kGemmThreads), 0, st, g);
@@ -138,15 +154,44 @@ int64_t conv_part_floats(const ConvGeom &g, int Cout) {
     const int64_t c = gemm_part_floats(Kc, P, Cout);                 // dcol
     if (b > m) m = b;
     if (c > m) m = c;
+    m = std::max(m, std::max(s3_part_floats(Cout, P, Kc), s3_part_floats(Cout, Kc, P)));   // implicit forms
     return m;
 }
+
+// Implicit-GEMM conv product on the split-bf16 kernel (A dense k-contiguous, B a conv loader),
+// with the same split-K / reduce tail as gemm().
+template <class LB>
+int gemm_s3_conv(const float *A, const LB &lb, float *C, const float *bias, const float *div, int M, int N, int K,
+                 float *part, int64_t part_cap, hipStream_t st) {
+    if (M <= 0 || N <= 0) return LRS_OK;
+    const Split s = choose_split(M, N, K, LRS_DIP_SPLIT_BF16, true);
+    GemmArgs g{A, nullptr, C, bias, div, M, N, K, s.kchunk, 0};
+    if (s.S > 1) {
+        if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
+        g.C = part;
+    }
+    dim3 grid((N + 127) / 128, (M + 127) / 128, s.S);
+    hipLaunchKernelGGL((k_gemm_s3<LdDense<true>, LB>), grid, dim3(kGemmThreads), 0, st, g, LdDense<true>{A, K, M}, lb);
+    if (s.S > 1) {
+        const int64_t MN = (int64_t)M * N;
+        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M,
+                           N, bias, div, 0, C);
+    }
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+inline bool conv_implicit_ok(const ConvGeom &g) { return g.k <= 3; }
 
 int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bias, int Cout, float *col, float *y,
              float *part, int64_t part_cap, hipStream_t st) {
     const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
     const float *B = x;
+    if (!plain_unit(g) && !col) {   // implicit im2col
+        if (!conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
+        return gemm_s3_conv(w, LdConvFwd{x, g, nullptr}, y, bias, nullptr, Cout, P, Kc, part, part_cap, st);
+    }
     if (!plain_unit(g)) {
-        if (!col) return LRS_E_WORKSPACE;
         const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min(Kc, 65535));
         hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, st, x, g, col);
         B = col;
@@ -155,10 +200,18 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
 }
 
 // gw = gz col^T / div ; gx = col2im(w^T gz) (gx nullable).  dcol: Kc*P floats when !plain.
+// implicit: `col` is the conv input x and col^T is gathered inside the GEMM.
 int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *w, const float *div, int Cout,
-             float *gx, float *gw, float *dcol, float *part, int64_t part_cap, hipStream_t st, int accum_gx = 0) {
+             float *gx, float *gw, float *dcol, float *part, int64_t part_cap, hipStream_t st, int accum_gx = 0,
+             bool implicit = false) {
     const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
-    int rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
+    int rc;
+    if (implicit && !plain_unit(g)) {
+        if (!conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
+        rc = gemm_s3_conv(gz, LdConvWgrad{col, g, Kc, nullptr}, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
+    } else {
+        rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
+    }
     if (rc || !gx) return rc;
     if (plain_unit(g)) return gemm(1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st, accum_gx);
     if (!dcol) return LRS_E_WORKSPACE;
@@ -321,6 +374,7 @@ extern "C" int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const f
     int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
     if (rc) return rc;
     if (!x || !w || !y || Cout <= 0) return LRS_E_INVALID;
+    if (!col && !plain_unit(g) && !conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
     const int64_t part = conv_part_floats(g, Cout);
     if (part > 0 && (!ws || ws_bytes < (size_t)part * sizeof(float))) return LRS_E_WORKSPACE;
     return conv_fwd(g, x, w, bias, Cout, col, y, (float *)ws, part, (hipStream_t)stream);
@@ -339,6 +393,22 @@ extern "C" int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float
     float *dc = dcol ? (float *)ws : nullptr;
     float *pt = (float *)ws + dcol;
     return conv_bwd(g, gy, col, w, w_div, Cout, gx, gw, dc, pt, part, (hipStream_t)stream);
+}
+
+extern "C" int lrs_conv2d_bwd_x_f32(const float *gy, const float *x, const float *w, const float *w_div, int Cin,
+                                    int H, int W, int Cout, int k, int stride, int pad, int pad_mode, int upsample,
+                                    float *gx, float *gw, void *ws, size_t ws_bytes, void *stream) {
+    ConvGeom g;
+    int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
+    if (rc) return rc;
+    if (!gy || !x || !w || !gw || Cout <= 0) return LRS_E_INVALID;
+    if (!conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
+    const int64_t part = conv_part_floats(g, Cout);
+    const int64_t dcol = plain_unit(g) ? 0 : (int64_t)Cin * k * k * g.Ho * g.Wo;
+    if (ws_bytes < (size_t)(part + dcol) * sizeof(float) || (!ws && part + dcol > 0)) return LRS_E_WORKSPACE;
+    float *dc = dcol ? (float *)ws : nullptr;
+    float *pt = (float *)ws + dcol;
+    return conv_bwd(g, gy, x, w, w_div, Cout, gx, gw, dc, pt, part, (hipStream_t)stream, 0, true);
 }
 
 extern "C" size_t lrs_bn_act_workspace(int C, int64_t P) {
@@ -494,6 +564,7 @@ struct lrs_dipnet {
     size_t ws_bytes = 0;
     int n_sn = 0;
     int64_t max_w = 0;
+    bool implicit = false;   // convs gather im2col inside the split-bf16 GEMM (no col buffers)
     float *params = nullptr, *grads = nullptr, *am = nullptr, *av = nullptr, *bnstats = nullptr;
     char *ws = nullptr;
     hipGraphExec_t gexec = nullptr;
@@ -592,8 +663,8 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
             const float *w = sn ? net->f(N.wn_off) : net->params + N.w_off;
             float *gx = t > 0 ? net->f(net->nodes[t - 1].grad_off) : nullptr;
             rc = conv_bwd(N.g, gz, colsrc, w, sn ? net->f(net->scale_off) + N.sn_index : nullptr, N.C, gx,
-                          net->grads + N.w_off, N.col_off >= 0 ? net->f(net->dcol_off) : nullptr,
-                          net->f(net->part_off), net->part_cap, st, t > 0 ? written[t] : 0);
+                          net->grads + N.w_off, !plain_unit(N.g) ? net->f(net->dcol_off) : nullptr,
+                          net->f(net->part_off), net->part_cap, st, t > 0 ? written[t] : 0, N.col_off < 0);
             if (rc) return rc;
             if (t > 0) written[t] = 1;
         } else if (N.d.kind == LRS_NODE_BN) {
@@ -662,6 +733,7 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     net->H = H;
     net->W = W;
     auto fail = [&](int rc) { delete net; return rc; };
+    net->implicit = g_dip_gemm_precision == LRS_DIP_SPLIT_BF16;
     int64_t pofs = 0, rofs = 0, ofs = 0, max_dz = 0, max_dcol = 0, part = 0, max_bnpart = 0;
     int n_sn = 0;
     for (int i = 0; i < n_nodes; ++i) {
@@ -690,7 +762,7 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                 if (N.C * N.Kc > net->max_w) net->max_w = N.C * N.Kc;
             }
             if (!plain_unit(N.g)) {
-                N.col_off = ofs; ofs += align64(N.Kc * N.P);
+                if (!(net->implicit && conv_implicit_ok(N.g))) { N.col_off = ofs; ofs += align64(N.Kc * N.P); }
                 if (N.Kc * N.P > max_dcol) max_dcol = N.Kc * N.P;
             }
             if (N.d.bn) { N.z_off = ofs; ofs += align64(N.C * N.P); }

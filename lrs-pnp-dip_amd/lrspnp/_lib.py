@@ -73,6 +73,8 @@ def _declare(L):
         "lrs_conv2d_fwd_f32": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, sz, vp]),
         "lrs_conv2d_bwd_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, sz,
                                      vp]),
+        "lrs_conv2d_bwd_x_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, sz,
+                                       vp]),
         "lrs_bn_act_workspace": (sz, [i32, i64]),
         "lrs_bn_act_fwd_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, f32, f32, vp, sz, vp]),
         "lrs_bn_act_bwd_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, vp, sz, vp]),

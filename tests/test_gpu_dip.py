@@ -114,6 +114,36 @@ def test_conv_fwd_bwd(L, case, precision):
     assert rel(gx, xr.grad) < 2e-5
 
 
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_implicit_fwd_bwd(L, case):
+    # col == NULL: the split-bf16 implicit-GEMM conv (im2col gathered in the kernel), and
+    # lrs_conv2d_bwd_x_f32 (dW's col^T gathered from x); same tolerances as the explicit path
+    cin, cout, H, W, k, stride, pad, pm, up = case
+    g = torch.Generator().manual_seed(hash(case) & 0xffff)
+    x = torch.randn(cin, H, W, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / np.sqrt(cin * k * k)
+    b = torch.randn(cout, generator=g) * 0.1
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yr = torch_conv(xr, wr, b, k, stride, pad, pm, up)
+    gy = torch.randn(yr.shape, generator=g)
+    yr.backward(gy)
+    xd, wd, bd, gyd = (t.cuda().contiguous() for t in (x, w, b, gy))
+    nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, stride, pad, up)
+    ws = torch.empty(nws // 4 + 1, device="cuda")
+    y = torch.full(yr.shape, float("nan"), device="cuda")
+    assert L.lrs_conv2d_fwd_f32(P(xd), cin, H, W, P(wd), P(bd), cout, k, stride, pad, pm, up,
+                                None, P(y), P(ws), nws, S()) == 0
+    assert rel(y, yr.detach()) < 1e-5
+    div = torch.tensor([1.7], device="cuda")
+    gw = torch.full_like(wd, float("nan"))
+    gx = torch.full_like(xd, float("nan"))
+    assert L.lrs_conv2d_bwd_x_f32(P(gyd), P(xd), P(wd), P(div), cin, H, W, cout, k, stride,
+                                  pad, pm, up, P(gx), P(gw), P(ws), nws, S()) == 0
+    torch.cuda.synchronize()
+    assert rel(gw, wr.grad / 1.7) < 2e-5
+    assert rel(gx, xr.grad) < 2e-5
+
+
 @pytest.mark.parametrize("bn,act,C,HW", [(1, 1, 128, 36 * 36), (1, 1, 64, 9), (0, 1, 198, 1296), (1, 2, 16, 100),
                                          (1, 1, 128, 196 * 196), (0, 1, 8, 50000)])
 def test_bn_act(L, bn, act, C, HW):

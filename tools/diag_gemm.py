@@ -24,7 +24,7 @@ SHAPES = [  # cin, cout, H, W, k, stride, pad, up  (196x196 U-Net, 512x512 skip 
 ]
 
 
-def run(shape, reps=10):
+def run(shape, reps=10, implicit=False):
     cin, cout, H, W, k, s, p, up = shape
     torch.manual_seed(0)
     x = torch.randn(cin, H, W, device="cuda")
@@ -41,14 +41,15 @@ def run(shape, reps=10):
     gx, gw = torch.empty_like(x), torch.empty_like(w)
     div = torch.ones(1, device="cuda")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    cp = P(col) if ncol else None
+    cp = P(col) if ncol and not implicit else None
 
     def fwd():
         assert L.lrs_conv2d_fwd_f32(P(x), cin, H, W, P(w), P(b), cout, k, s, p, 1, up, cp, P(y), P(ws), nws, st) == 0
 
     def bwd():
-        assert L.lrs_conv2d_bwd_f32(P(gy), cp if ncol else P(x), P(w), P(div), cin, H, W, cout, k, s, p, 1, up,
-                                    P(gx), P(gw), P(ws), nws, st) == 0
+        fn = L.lrs_conv2d_bwd_x_f32 if implicit else L.lrs_conv2d_bwd_f32
+        assert fn(P(gy), cp if cp is not None else P(x), P(w), P(div), cin, H, W, cout, k, s, p, 1, up,
+                  P(gx), P(gw), P(ws), nws, st) == 0
     out = []
     for f in (fwd, bwd):
         f(); torch.cuda.synchronize()
@@ -67,8 +68,13 @@ for sh in SHAPES[int(os.environ.get('DIAG_FIRST', 0)):]:
     for prec, name in ((0, "f32"), (1, "b3")):
         L.lrs_dip_set_precision(prec)
         res[name] = run(sh)
+    res["imp"] = run(sh, implicit=True)
     (tf, tb), fl, o32 = res["f32"]
     (bf, bb), _, ob3 = res["b3"]
     err = [float((a - c).norm() / c.norm()) for a, c in zip(ob3, o32)]
     print(f"{sh}: fwd f32 {tf:8.1f} us b3 {bf:8.1f} us ({fl / bf / 1e6:6.1f} TF/s) | bwd f32 {tb:8.1f} b3 {bb:8.1f} us "
           f"({2 * fl / bb / 1e6:6.1f} TF/s) | rel diff y/gx/gw {err[0]:.1e} {err[1]:.1e} {err[2]:.1e}", flush=True)
+    (tf, tb), _, oim = res["imp"]
+    err = [float((a - c).norm() / c.norm()) for a, c in zip(oim, o32)]
+    print(f"    implicit: fwd {tf:8.1f} us ({fl / tf / 1e6:6.1f} TF/s) bwd {tb:8.1f} us ({2 * fl / tb / 1e6:6.1f} TF/s)"
+          f" | rel diff {err[0]:.1e} {err[1]:.1e} {err[2]:.1e}", flush=True)
