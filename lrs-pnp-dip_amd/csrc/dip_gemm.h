@@ -174,6 +174,72 @@ struct LdConvFwd {
     }
 };
 
+// Data-gradient operands (stride 1): gxp[ci][q] over the padded, upsampled domain
+// q = (iy, ix) in [0, Hu + 2 pad) x [0, Wu + 2 pad) is the correlation of gy with the kernel,
+//   gxp[ci][iy][ix] = sum_{co, ky, kx} W[co][ci][ky][kx] gy[co][iy - ky][ix - kx],
+// an implicit GEMM with M = Cin, K = (co, ky, kx), N = q; k_fold_pad then adds the padded
+// border back onto the pixels it mirrors and sums the x2 upsample (the adjoint of the gather
+// of LdConvFwd), so no Kc x P col gradient is ever written.
+// A: W^T, row ci, k index (co, kyx) -> W[co][ci][kyx]
+struct LdWT {
+    static constexpr bool kc = true;
+    const float *W;
+    int Cin, kk;
+    __device__ __forceinline__ void setup(int, int *) {}
+    __device__ __forceinline__ void load(int x0, int k0, int kend, float (&v)[16]) const {
+        const int ci = x0 + s3_row<true>(), kb = k0 + s3_kb<true>();
+        int co = kb / kk, kyx = kb - co * kk;
+        const int Kc = Cin * kk;
+        const float *src = W + (int64_t)co * Kc + ci * kk;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            v[u] = (ci < Cin && kb + u < kend) ? src[kyx] : 0.0f;
+            if (++kyx == kk) {
+                kyx = 0;
+                src += Kc;
+            }
+        }
+    }
+};
+
+// B: gy gathered at (iy - ky, ix - kx); k index (co, kyx), x index q.  Offsets per (kyx, q) of
+// the workgroup's 128 q tabulated once, as in LdConvFwd.
+struct LdConvDgrad {
+    static constexpr bool kc = false;
+    const float *GY;
+    ConvGeom g;
+    int *tab;
+    __device__ __forceinline__ void setup(int x0, int *smem) {
+        tab = smem;
+        const int kk = g.k * g.k, Wp = g.Wu + 2 * g.pad, Q = (g.Hu + 2 * g.pad) * Wp;
+        for (int i = threadIdx.x; i < kk * 128; i += blockDim.x) {
+            const int kyx = i >> 7, q = x0 + (i & 127);
+            int o = -1;
+            if (q < Q) {
+                const int iy = q / Wp, ix = q - iy * Wp, ky = kyx / g.k, kx = kyx - ky * g.k;
+                const int oy = iy - ky, ox = ix - kx;
+                if (oy >= 0 && oy < g.Ho && ox >= 0 && ox < g.Wo) o = oy * g.Wo + ox;
+            }
+            tab[i] = o;
+        }
+    }
+    __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
+        const int x = s3_row<false>(), r0 = k0 + s3_kb<false>();
+        const int kk = g.k * g.k, plane = g.Ho * g.Wo;
+        int c = r0 / kk, kyx = r0 - c * kk;
+        const float *base = GY + (int64_t)c * plane;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int o = tab[kyx * 128 + x];
+            v[u] = (r0 + u < kend && o >= 0) ? base[o] : 0.0f;
+            if (++kyx == kk) {
+                kyx = 0;
+                base += plane;
+            }
+        }
+    }
+};
+
 // Weight-gradient B operand: col^T, x index r = (c, ky, kx) (an output column of dW), k index p
 // = output pixel (stored "[x][k]").  A thread's row r is fixed for the whole kernel; the source
 // offsets of the step's 32 pixels for every (ky, kx) are tabulated in LDS one step ahead
@@ -301,6 +367,33 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
                 }
             }
         }
+}
+
+// gx[c][sy][sx] (+)= sum over the x2 upsample children u of sum over the padded positions that
+// read u (direct + reflection mirrors, padded_sources) of gxp[c][iy][ix]
+__global__ __launch_bounds__(256) void k_fold_pad(const float *__restrict__ gxp, ConvGeom gm, float *__restrict__ gx,
+                                                  int accum) {
+    const int HW = gm.Hs * gm.Ws, Wp = gm.Wu + 2 * gm.pad, Qp = (gm.Hu + 2 * gm.pad) * Wp;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= HW) return;
+    const int sy = q / gm.Ws, sx = q - sy * gm.Ws;
+    const int nup = gm.up ? 2 : 1;
+    for (int c = blockIdx.y; c < gm.Cin; c += gridDim.y) {
+        const float *src = gxp + (int64_t)c * Qp;
+        float acc = 0.0f;
+        for (int a = 0; a < nup; ++a) {
+            int iys[3];
+            const int ny = padded_sources(gm.up ? 2 * sy + a : sy, gm.Hu, gm.pad, gm.pad_mode, iys);
+            for (int b = 0; b < nup; ++b) {
+                int ixs[3];
+                const int nx = padded_sources(gm.up ? 2 * sx + b : sx, gm.Wu, gm.pad, gm.pad_mode, ixs);
+                for (int py = 0; py < ny; ++py)
+                    for (int px = 0; px < nx; ++px) acc += src[iys[py] * Wp + ixs[px]];
+            }
+        }
+        const int64_t i = (int64_t)c * HW + q;
+        gx[i] = accum ? gx[i] + acc : acc;
+    }
 }
 
 }  // namespace lrs

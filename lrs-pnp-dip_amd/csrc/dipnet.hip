@@ -155,23 +155,25 @@ int64_t conv_part_floats(const ConvGeom &g, int Cout) {
     if (b > m) m = b;
     if (c > m) m = c;
     m = std::max(m, std::max(s3_part_floats(Cout, P, Kc), s3_part_floats(Cout, Kc, P)));   // implicit forms
+    const int Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad);
+    m = std::max(m, s3_part_floats(g.Cin, Qp, Cout * g.k * g.k));                           // transposed
     return m;
 }
 
 // Implicit-GEMM conv product on the split-bf16 kernel (A dense k-contiguous, B a conv loader),
 // with the same split-K / reduce tail as gemm().
-template <class LB>
-int gemm_s3_conv(const float *A, const LB &lb, float *C, const float *bias, const float *div, int M, int N, int K,
+template <class LA, class LB>
+int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const float *div, int M, int N, int K,
                  float *part, int64_t part_cap, hipStream_t st) {
     if (M <= 0 || N <= 0) return LRS_OK;
     const Split s = choose_split(M, N, K, LRS_DIP_SPLIT_BF16, true);
-    GemmArgs g{A, nullptr, C, bias, div, M, N, K, s.kchunk, 0};
+    GemmArgs g{nullptr, nullptr, C, bias, div, M, N, K, s.kchunk, 0};
     if (s.S > 1) {
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
         g.C = part;
     }
     dim3 grid((N + 127) / 128, (M + 127) / 128, s.S);
-    hipLaunchKernelGGL((k_gemm_s3<LdDense<true>, LB>), grid, dim3(kGemmThreads), 0, st, g, LdDense<true>{A, K, M}, lb);
+    hipLaunchKernelGGL((k_gemm_s3<LA, LB>), grid, dim3(kGemmThreads), 0, st, g, la, lb);
     if (s.S > 1) {
         const int64_t MN = (int64_t)M * N;
         hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M,
@@ -189,7 +191,8 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
     const float *B = x;
     if (!plain_unit(g) && !col) {   // implicit im2col
         if (!conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
-        return gemm_s3_conv(w, LdConvFwd{x, g, nullptr}, y, bias, nullptr, Cout, P, Kc, part, part_cap, st);
+        return gemm_s3_conv(LdDense<true>{w, Kc, Cout}, LdConvFwd{x, g, nullptr}, y, bias, nullptr, Cout, P, Kc, part,
+                            part_cap, st);
     }
     if (!plain_unit(g)) {
         const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min(Kc, 65535));
@@ -208,13 +211,26 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
     int rc;
     if (implicit && !plain_unit(g)) {
         if (!conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
-        rc = gemm_s3_conv(gz, LdConvWgrad{col, g, Kc, nullptr}, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
+        rc = gemm_s3_conv(LdDense<true>{gz, P, Cout}, LdConvWgrad{col, g, Kc, nullptr}, gw, nullptr, div, Cout, Kc, P,
+                          part, part_cap, st);
     } else {
         rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
     }
     if (rc || !gx) return rc;
     if (plain_unit(g)) return gemm(1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st, accum_gx);
     if (!dcol) return LRS_E_WORKSPACE;
+    const int Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad);
+    if (implicit && g.stride == 1 && (int64_t)g.Cin * Qp <= (int64_t)Kc * P) {
+        // gxp = W^T (x) gz over the padded domain (implicit, in the dcol space), then fold the
+        // padding / upsample
+        rc = gemm_s3_conv(LdWT{w, g.Cin, g.k * g.k}, LdConvDgrad{gz, g, nullptr}, dcol, nullptr, nullptr, g.Cin, Qp,
+                          Cout * g.k * g.k, part, part_cap, st);
+        if (rc) return rc;
+        const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
+        hipLaunchKernelGGL(k_fold_pad, grid, dim3(256), 0, st, dcol, g, gx, accum_gx);
+        LRS_CHECK_LAUNCH();
+        return LRS_OK;
+    }
     rc = gemm(1, 0, w, gz, dcol, nullptr, nullptr, Kc, P, Cout, part, part_cap, st);
     if (rc) return rc;
     const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
