@@ -69,14 +69,17 @@ Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision, bo
     // long-K GEMMs (the weight gradients, K = pixels) take 128-tiles with deep split-K on the
     // split-bf16 path when that still gives >= 256 workgroups (measured 25-30 % faster at 196^2 and
     // 512^2; the 1x1 layer's 2-tile gradient is faster on 64-tiles)
-    const bool big = force_big || t128 >= 64 || (precision == LRS_DIP_SPLIT_BF16 && K >= 8192 && t128 >= 4);
+    // Very long K with few tiles (a 1x1 conv's weight gradient over 512^2 pixels) splits up to 256
+    // ways on the split-bf16 path, keeping >= 16 k-steps per workgroup.
+    const bool deep = precision == LRS_DIP_SPLIT_BF16 && K >= 65536;
+    const bool big = force_big || t128 >= 64 || (precision == LRS_DIP_SPLIT_BF16 && K >= 8192 && t128 >= 4) || deep;
     const int64_t tiles = big ? t128 : (int64_t)((M + kBM64 - 1) / kBM64) * ((N + kBN64 - 1) / kBN64);
     int S = 1;
     if (tiles < 256) {
         S = (int)((512 + tiles - 1) / tiles);
-        const int smax = (K + 127) / 128;
+        const int smax = deep ? K / 512 : (K + 127) / 128;
         if (S > smax) S = smax;
-        if (S > 64) S = 64;
+        if (S > (deep ? 256 : 64)) S = deep ? 256 : 64;
         if (S < 1) S = 1;
     }
     const int bk = (big && precision == LRS_DIP_SPLIT_BF16) ? kBK32 : kBK;

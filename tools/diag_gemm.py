@@ -21,6 +21,9 @@ SHAPES = [  # cin, cout, H, W, k, stride, pad, up  (196x196 U-Net, 512x512 skip 
     (224, 128, 512, 512, 3, 2, 1, 0),
     (128, 128, 256, 256, 3, 1, 1, 0),
     (132, 128, 512, 512, 3, 1, 1, 0),
+    (128, 128, 512, 512, 1, 1, 0, 0),
+    (256, 128, 512, 512, 1, 1, 0, 0),
+    (128, 4, 512, 512, 1, 1, 0, 0),
 ]
 
 
