@@ -12,10 +12,12 @@
 // ds_read_b128.  One LDS stage, the next step's global loads in registers during the MFMAs,
 // 2-3 workgroups per CU.  gridDim.z > 1 = split-K as in k_gemm.
 //
-// Operands come from loaders: dense matrices, or the implicit im2col of a conv (reflection /
-// zero padding, stride and the nearest x2 upsample folded into the gather), so the forward and
-// the weight gradient of a conv never materialise the col matrix (the reference's
-// ReflectionPad2d + Conv2d, lipschitz_constraint_layer.py:65-78, common.py:73-121).
+// Operands come from loaders: dense fp32 matrices (split at the LDS store), conv weights
+// pre-split into bf16 planes once per step (k_wprep: no split work in the GEMM), or the implicit
+// im2col of a conv (reflection / zero padding, stride and the nearest x2 upsample folded into
+// LDS offset tables, buffer loads with range-checked zero fill), so no conv direction
+// materialises a col matrix (the reference's ReflectionPad2d + Conv2d,
+// lipschitz_constraint_layer.py:65-78, common.py:73-121).
 #pragma once
 
 #include "lrs_dip.h"
@@ -99,6 +101,7 @@ __device__ __forceinline__ s3f4 s3_mfma6(const s3bf8 (&A)[3], const s3bf8 (&B)[3
 template <bool KC>
 struct LdDense {
     static constexpr bool kc = KC;
+    static constexpr bool pre = false;
     const float *S;
     int ld, X;
     __device__ __forceinline__ void setup(int, int *) {}
@@ -134,153 +137,187 @@ __device__ __forceinline__ int conv_src(int u, int n, int mode, int up) {
     return up ? (u >> 1) : u;
 }
 
-// Forward B operand: col[r][p] with r = (c, ky, kx) the k index and p = output pixel the x
-// index (stored "[k][x]").  The k*k source offsets of the workgroup's 128 pixels are tabulated
-// in LDS once; a step then costs one table read + one gather per value.
-struct LdConvFwd {
+// ---- implicit-GEMM conv operands --------------------------------------------------------------
+// The conv's K index is tap-major, r = kyx * Cp + c (kyx = ky * k + kx, c < Cp = Cin rounded up to
+// 16, channels >= Cin are zero), so the 16 consecutive k a thread loads share one tap: their
+// source offset is one LDS table entry and the 16 channels are a scalar stride apart.  Sources
+// are read through buffer loads (32-bit offsets, range-checked): a table entry kOob marks a zero
+// pad / out-of-range pixel and the hardware returns 0 for it, so no per-value select remains.
+constexpr int kOob = 0x7FFFFFF0;   // >= every buffer's byte count (host checks < kOob)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s3_rsrc(const void *p, int bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const void *u = reinterpret_cast<const void *>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(u), 0, __builtin_amdgcn_readfirstlane(bytes),
+                                             0x00020000);
+}
+
+__device__ __forceinline__ float s3_bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+// Pre-split operand (the conv weights, split into bf16 planes by k_wprep): plane p of row x at
+// P + p * pstride + x * ld, k contiguous.  Loads go straight to the LDS image (no split).
+struct RegP {
+    uint4 h[3][2];
+};
+
+struct LdPre {
+    static constexpr bool kc = true;
+    static constexpr bool pre = true;
+    const __bf16 *P;
+    int64_t pstride;
+    int ld, X;
+    __device__ __forceinline__ void setup(int, int *) {}
+    __device__ __forceinline__ void load(int x0, int k0, int kend, RegP &r) const {
+        const int x = x0 + s3_row<true>(), kb = k0 + s3_kb<true>();
+        const bool ok = x < X && kb < kend;   // K and kend are multiples of 16
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(P + p * pstride + (int64_t)x * ld + kb);
+            r.h[p][0] = ok ? src[0] : uint4{0, 0, 0, 0};
+            r.h[p][1] = ok ? src[1] : uint4{0, 0, 0, 0};
+        }
+    }
+};
+
+__device__ __forceinline__ void s3_store_pre(S3Tile &T, const RegP &r) {
+    const int row = s3_row<true>(), c0 = s3_kb<true>() >> 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int ch = s3_chunk(row, c0 + h) * 8;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint4 *>(&T.v[p][row][ch]) = r.h[p][h];
+    }
+}
+
+// Forward B: col[r][p] (k = r tap-major, x = output pixel p).  Table [kk][128] of the
+// workgroup's pixels' source byte offsets within a channel plane.
+struct LdFwdTM {
     static constexpr bool kc = false;
+    static constexpr bool pre = false;
     const float *X;
+    int xbytes;
     ConvGeom g;
-    int *tab;   // [k*k][128] source offset in a channel plane, -1 = zero pad / past P
+    int Cp;
+    int *tab;
     __device__ __forceinline__ void setup(int x0, int *smem) {
         tab = smem;
         const int kk = g.k * g.k, P = g.Ho * g.Wo;
         for (int i = threadIdx.x; i < kk * 128; i += blockDim.x) {
             const int kyx = i >> 7, p = x0 + (i & 127);
-            int o = -1;
+            int o = kOob;
             if (p < P) {
                 const int oy = p / g.Wo, ox = p - oy * g.Wo, ky = kyx / g.k, kx = kyx - ky * g.k;
                 const int sy = conv_src(oy * g.stride + ky - g.pad, g.Hu, g.pad_mode, g.up);
                 const int sx = conv_src(ox * g.stride + kx - g.pad, g.Wu, g.pad_mode, g.up);
-                if (sy >= 0 && sx >= 0) o = sy * g.Ws + sx;
+                if (sy >= 0 && sx >= 0) o = 4 * (sy * g.Ws + sx);
             }
             tab[i] = o;
         }
     }
     __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
-        const int x = s3_row<false>(), r0 = k0 + s3_kb<false>();
-        const int kk = g.k * g.k, plane = g.Hs * g.Ws;
-        int c = r0 / kk, kyx = r0 - c * kk;
-        const float *base = X + (int64_t)c * plane;
+        const int r0 = __builtin_amdgcn_readfirstlane(k0 + s3_kb<false>());
+        if (r0 >= kend) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int o = tab[kyx * 128 + x];
-            v[u] = (r0 + u < kend && o >= 0) ? base[o] : 0.0f;
-            if (++kyx == kk) {
-                kyx = 0;
-                base += plane;
-            }
+            for (int u = 0; u < 16; ++u) v[u] = 0.0f;
+            return;
         }
+        const int kyx = r0 / Cp, c0 = r0 - kyx * Cp;
+        const int pb = g.Hs * g.Ws * 4;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
+        const int vo = tab[kyx * 128 + s3_row<false>()];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = c0 + u < g.Cin ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
     }
 };
 
-// Data-gradient operands (stride 1): gxp[ci][q] over the padded, upsampled domain
-// q = (iy, ix) in [0, Hu + 2 pad) x [0, Wu + 2 pad) is the correlation of gy with the kernel,
-//   gxp[ci][iy][ix] = sum_{co, ky, kx} W[co][ci][ky][kx] gy[co][iy - ky][ix - kx],
-// an implicit GEMM with M = Cin, K = (co, ky, kx), N = q; k_fold_pad then adds the padded
-// border back onto the pixels it mirrors and sums the x2 upsample (the adjoint of the gather
-// of LdConvFwd), so no Kc x P col gradient is ever written.
-// A: W^T, row ci, k index (co, kyx) -> W[co][ci][kyx]
-struct LdWT {
-    static constexpr bool kc = true;
-    const float *W;
-    int Cin, kk;
-    __device__ __forceinline__ void setup(int, int *) {}
-    __device__ __forceinline__ void load(int x0, int k0, int kend, float (&v)[16]) const {
-        const int ci = x0 + s3_row<true>(), kb = k0 + s3_kb<true>();
-        int co = kb / kk, kyx = kb - co * kk;
-        const int Kc = Cin * kk;
-        const float *src = W + (int64_t)co * Kc + ci * kk;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            v[u] = (ci < Cin && kb + u < kend) ? src[kyx] : 0.0f;
-            if (++kyx == kk) {
-                kyx = 0;
-                src += Kc;
-            }
-        }
-    }
-};
-
-// B: gy gathered at (iy - ky, ix - kx); k index (co, kyx), x index q.  Offsets per (kyx, q) of
-// the workgroup's 128 q tabulated once, as in LdConvFwd.
-struct LdConvDgrad {
+// Data-gradient B (stride 1): gy at (iy - ky, ix - kx) over the padded, upsampled domain
+// q = (iy, ix); k = kyx * Cop + co.  Table [kk][128] of the workgroup's q.
+struct LdDgradTM {
     static constexpr bool kc = false;
+    static constexpr bool pre = false;
     const float *GY;
+    int gbytes;
     ConvGeom g;
+    int Cout, Cop;
     int *tab;
     __device__ __forceinline__ void setup(int x0, int *smem) {
         tab = smem;
         const int kk = g.k * g.k, Wp = g.Wu + 2 * g.pad, Q = (g.Hu + 2 * g.pad) * Wp;
         for (int i = threadIdx.x; i < kk * 128; i += blockDim.x) {
             const int kyx = i >> 7, q = x0 + (i & 127);
-            int o = -1;
+            int o = kOob;
             if (q < Q) {
                 const int iy = q / Wp, ix = q - iy * Wp, ky = kyx / g.k, kx = kyx - ky * g.k;
                 const int oy = iy - ky, ox = ix - kx;
-                if (oy >= 0 && oy < g.Ho && ox >= 0 && ox < g.Wo) o = oy * g.Wo + ox;
+                if (oy >= 0 && oy < g.Ho && ox >= 0 && ox < g.Wo) o = 4 * (oy * g.Wo + ox);
             }
             tab[i] = o;
         }
     }
     __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
-        const int x = s3_row<false>(), r0 = k0 + s3_kb<false>();
-        const int kk = g.k * g.k, plane = g.Ho * g.Wo;
-        int c = r0 / kk, kyx = r0 - c * kk;
-        const float *base = GY + (int64_t)c * plane;
+        const int r0 = __builtin_amdgcn_readfirstlane(k0 + s3_kb<false>());
+        if (r0 >= kend) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int o = tab[kyx * 128 + x];
-            v[u] = (r0 + u < kend && o >= 0) ? base[o] : 0.0f;
-            if (++kyx == kk) {
-                kyx = 0;
-                base += plane;
-            }
+            for (int u = 0; u < 16; ++u) v[u] = 0.0f;
+            return;
         }
+        const int kyx = r0 / Cop, c0 = r0 - kyx * Cop;
+        const int pb = g.Ho * g.Wo * 4;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(GY, gbytes);
+        const int vo = tab[kyx * 128 + s3_row<false>()];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = c0 + u < Cout ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
     }
 };
 
-// Weight-gradient B operand: col^T, x index r = (c, ky, kx) (an output column of dW), k index p
-// = output pixel (stored "[x][k]").  A thread's row r is fixed for the whole kernel; the source
-// offsets of the step's 32 pixels for every (ky, kx) are tabulated in LDS one step ahead
-// (prepare(), double-buffered), so a value costs one table read and one gather.
-struct LdConvWgrad {
+// Weight-gradient B: col^T, x = r = c * kk + kyx (dW's own column order: a wave's 32 rows are
+// ~4 channels x all taps, whose gathers share cache lines), k = output pixel.  The thread's row
+// is fixed; the step's 32 pixels x kk taps are tabulated one step ahead (prepare,
+// double-buffered).  Rows past Cin * kk read at kOob (zeros).
+struct LdWgradTM {
     static constexpr bool kc = true;
-    static constexpr bool kPrepare = true;
+    static constexpr bool pre = false;
     const float *X;
+    int xbytes;
     ConvGeom g;
-    int Kc;
-    int *tab;   // [2][k*k][32]
-    __device__ __forceinline__ void setup(int, int *smem) { tab = smem; }
-    // table of the step starting at k0 into buffer b
+    int *tab;   // [2][kk][32]
+    int trow, cbase;
+    __device__ __forceinline__ void setup(int x0, int *smem) {
+        tab = smem;
+        const int r = x0 + s3_row<true>(), kk = g.k * g.k;
+        const int c = r / kk, kyx = r - c * kk;
+        const bool ok = c < g.Cin;
+        trow = (ok ? kyx : 0) * 32 + s3_kb<true>();
+        cbase = ok ? c * g.Hs * g.Ws * 4 : kOob;
+    }
     __device__ __forceinline__ void prepare(int k0, int kend, int b) const {
         const int kk = g.k * g.k;
         for (int i = threadIdx.x; i < kk * 32; i += blockDim.x) {
             const int kyx = i >> 5, p = k0 + (i & 31);
-            int o = -1;
+            int o = kOob;
             if (p < kend) {
                 const int oy = p / g.Wo, ox = p - oy * g.Wo, ky = kyx / g.k, kx = kyx - ky * g.k;
                 const int sy = conv_src(oy * g.stride + ky - g.pad, g.Hu, g.pad_mode, g.up);
                 const int sx = conv_src(ox * g.stride + kx - g.pad, g.Wu, g.pad_mode, g.up);
-                if (sy >= 0 && sx >= 0) o = sy * g.Ws + sx;
+                if (sy >= 0 && sx >= 0) o = 4 * (sy * g.Ws + sx);
             }
             tab[b * 9 * 32 + i] = o;
         }
     }
-    __device__ __forceinline__ void load(int x0, int k0, int kend, float (&v)[16], int b) const {
-        const int r = x0 + s3_row<true>(), kb = s3_kb<true>();
-        const int kk = g.k * g.k;
-        const int c = r / kk, kyx = r - c * kk;
-        const float *pl = X + (int64_t)c * g.Hs * g.Ws;
-        const int *t = tab + b * 9 * 32 + (r < Kc ? kyx : 0) * 32 + kb;
-        int o[16];
+    __device__ __forceinline__ void load(int, int, int, float (&v)[16], int b) const {
+        const int *t = tab + b * 9 * 32 + trow;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int4 f = *reinterpret_cast<const int4 *>(t + 4 * q);
-            o[4 * q] = f.x; o[4 * q + 1] = f.y; o[4 * q + 2] = f.z; o[4 * q + 3] = f.w;
+            v[4 * q] = s3_bload(rs, f.x + cbase, 0);
+            v[4 * q + 1] = s3_bload(rs, f.y + cbase, 0);
+            v[4 * q + 2] = s3_bload(rs, f.z + cbase, 0);
+            v[4 * q + 3] = s3_bload(rs, f.w + cbase, 0);
         }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = (r < Kc && o[u] >= 0) ? pl[o[u]] : 0.0f;
     }
 };
 
@@ -289,7 +326,7 @@ struct HasPrepare {
     static constexpr bool value = false;
 };
 template <>
-struct HasPrepare<LdConvWgrad> {
+struct HasPrepare<LdWgradTM> {
     static constexpr bool value = true;
 };
 
@@ -316,19 +353,24 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = s3f4{0.f, 0.f, 0.f, 0.f};
     float va[16], vb[16];
-    la.load(m0, kbeg, kend, va);
+    RegP pa;   // LA::pre: the weight planes
+    static_assert(!LB::pre, "B is never pre-split");
+    if constexpr (LA::pre) la.load(m0, kbeg, kend, pa);
+    else la.load(m0, kbeg, kend, va);
     if constexpr (PREP) lb.load(n0, kbeg, kend, vb, 0);
     else lb.load(n0, kbeg, kend, vb);
     int tb = 0;
     for (int k0 = kbeg; k0 < kend; k0 += kS3K) {
-        s3_store<LA::kc>(As, va);
+        if constexpr (LA::pre) s3_store_pre(As, pa);
+        else s3_store<LA::kc>(As, va);
         s3_store<LB::kc>(Bs, vb);
         if constexpr (PREP) {
             if (k0 + kS3K < kend) lb.prepare(k0 + kS3K, kend, tb ^ 1);
         }
         __syncthreads();
         if (k0 + kS3K < kend) {
-            la.load(m0, k0 + kS3K, kend, va);
+            if constexpr (LA::pre) la.load(m0, k0 + kS3K, kend, pa);
+            else la.load(m0, k0 + kS3K, kend, va);
             if constexpr (PREP) lb.load(n0, k0 + kS3K, kend, vb, tb ^ 1);
             else lb.load(n0, k0 + kS3K, kend, vb);
         }
@@ -367,6 +409,35 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
                 }
             }
         }
+}
+
+// Per conv weight W [Cout][Cin][kk] (fp32): the three bf16 planes of the forward operand
+// WF[p][co][kyx * Cp + c] and of the data-gradient operand WD[p][ci][kyx * Cop + co]
+// (Cp, Cop: Cin, Cout rounded up to 16; padding zero).  WD nullable.
+__global__ __launch_bounds__(256) void k_wprep(const float *__restrict__ W, int Cout, int Cin, int kk, int Cp, int Cop,
+                                               __bf16 *__restrict__ WF, __bf16 *__restrict__ WD) {
+    const int64_t nf = (int64_t)Cout * kk * Cp, nd = WD ? (int64_t)Cin * kk * Cop : 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf + nd; i += (int64_t)gridDim.x * blockDim.x) {
+        float x;
+        __bf16 *dst;
+        int64_t plane, j;
+        if (i < nf) {
+            const int co = (int)(i / (kk * Cp)), rem = (int)(i - (int64_t)co * kk * Cp);
+            const int kyx = rem / Cp, c = rem - kyx * Cp;
+            x = c < Cin ? W[((int64_t)co * Cin + c) * kk + kyx] : 0.0f;
+            dst = WF; plane = nf; j = i;
+        } else {
+            j = i - nf;
+            const int ci = (int)(j / (kk * Cop)), rem = (int)(j - (int64_t)ci * kk * Cop);
+            const int kyx = rem / Cop, co = rem - kyx * Cop;
+            x = co < Cout ? W[((int64_t)co * Cin + ci) * kk + kyx] : 0.0f;
+            dst = WD; plane = nd;
+        }
+        const S3Split q = s3_split(x);
+        dst[j] = q.b0;
+        dst[plane + j] = q.b1;
+        dst[2 * plane + j] = q.b2;
+    }
 }
 
 // gx[c][sy][sx] (+)= sum over the x2 upsample children u of sum over the padded positions that

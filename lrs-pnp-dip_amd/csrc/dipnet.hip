@@ -150,21 +150,31 @@ int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *
     return LRS_OK;
 }
 
+inline int r16(int x) { return (x + 15) & ~15; }
+
 int64_t conv_part_floats(const ConvGeom &g, int Cout) {
-    const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
+    const int P = g.Ho * g.Wo, kk = g.k * g.k, Kc = g.Cin * kk;
     int64_t m = gemm_part_floats(Cout, P, Kc);                       // forward
     const int64_t b = gemm_part_floats(Cout, Kc, P);                 // dW
     const int64_t c = gemm_part_floats(Kc, P, Cout);                 // dcol
     if (b > m) m = b;
     if (c > m) m = c;
-    m = std::max(m, std::max(s3_part_floats(Cout, P, Kc), s3_part_floats(Cout, Kc, P)));   // implicit forms
+    // implicit forms (tap-major K, channels rounded up to 16)
+    m = std::max(m, std::max(s3_part_floats(Cout, P, kk * r16(g.Cin)), s3_part_floats(Cout, Kc, P)));
     const int Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad);
-    m = std::max(m, s3_part_floats(g.Cin, Qp, Cout * g.k * g.k));                           // transposed
+    m = std::max(m, s3_part_floats(g.Cin, Qp, kk * r16(Cout)));
     return m;
 }
 
-// Implicit-GEMM conv product on the split-bf16 kernel (A dense k-contiguous, B a conv loader),
-// with the same split-K / reduce tail as gemm().
+// bf16 elements of a conv's pre-split weight planes: forward operand WF [3][Cout][kk*Cp], then
+// the data-gradient operand WD [3][Cin][kk*Cop]
+inline int64_t wprep_fwd_elems(const ConvGeom &g, int Cout) { return 3 * (int64_t)Cout * g.k * g.k * r16(g.Cin); }
+inline int64_t wprep_elems(const ConvGeom &g, int Cout) {
+    return wprep_fwd_elems(g, Cout) + 3 * (int64_t)g.Cin * g.k * g.k * r16(Cout);
+}
+
+// Implicit-GEMM conv product on the split-bf16 kernel, with the same split-K / reduce tail as
+// gemm().
 template <class LA, class LB>
 int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const float *div, int M, int N, int K,
                  float *part, int64_t part_cap, hipStream_t st) {
@@ -179,14 +189,17 @@ int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const 
     hipLaunchKernelGGL((k_gemm_s3<LA, LB>), grid, dim3(kGemmThreads), 0, st, g, la, lb);
     if (s.S > 1) {
         const int64_t MN = (int64_t)M * N;
-        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M,
-                           N, bias, div, 0, C);
+        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M, N,
+                           bias, div, 0, C);
     }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
 
-inline bool conv_implicit_ok(const ConvGeom &g) { return g.k <= 3; }
+// implicit GEMM: k <= 3 (LDS tables) and both operand tensors addressable by 32-bit buffer offsets
+inline bool conv_implicit_ok(const ConvGeom &g, int Cout) {
+    return g.k <= 3 && (int64_t)g.Cin * g.Hs * g.Ws * 4 < kOob && (int64_t)Cout * g.Ho * g.Wo * 4 < kOob;
+}
 
 // The engine runs a conv as an implicit GEMM from this many output pixels up; below it the maps
 // are small enough that an explicit im2col into a cached col buffer plus the 64-tile GEMMs is
@@ -197,14 +210,26 @@ inline int64_t implicit_min_pixels() {
     return v;
 }
 
+// split w into the bf16 planes of the forward operand (and of the data-gradient one if wd)
+void wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, hipStream_t st) {
+    const int kk = g.k * g.k;
+    const int64_t n = wprep_elems(g, Cout) / 3;
+    hipLaunchKernelGGL(k_wprep, dim3(ew_blocks(n, 2048)), dim3(256), 0, st, w, Cout, g.Cin, kk, r16(g.Cin), r16(Cout),
+                       wf, wd);
+}
+
+// y = conv(x) + bias.  Explicit (col != NULL): im2col + GEMM.  Implicit (col == NULL, wpre =
+// the weight planes from wprep): tap-major implicit GEMM.
 int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bias, int Cout, float *col, float *y,
-             float *part, int64_t part_cap, hipStream_t st) {
+             float *part, int64_t part_cap, hipStream_t st, const __bf16 *wpre = nullptr) {
     const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
     const float *B = x;
     if (!plain_unit(g) && !col) {   // implicit im2col
-        if (!conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
-        return gemm_s3_conv(LdDense<true>{w, Kc, Cout}, LdConvFwd{x, g, nullptr}, y, bias, nullptr, Cout, P, Kc, part,
-                            part_cap, st);
+        if (!conv_implicit_ok(g, Cout) || !wpre) return LRS_E_UNSUPPORTED;
+        const int kk = g.k * g.k, Cp = r16(g.Cin);
+        return gemm_s3_conv(LdPre{wpre, (int64_t)Cout * kk * Cp, kk * Cp, Cout},
+                            LdFwdTM{x, g.Cin * g.Hs * g.Ws * 4, g, Cp, nullptr}, y, bias, nullptr, Cout, P, kk * Cp,
+                            part, part_cap, st);
     }
     if (!plain_unit(g)) {
         const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min(Kc, 65535));
@@ -215,16 +240,18 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
 }
 
 // gw = gz col^T / div ; gx = col2im(w^T gz) (gx nullable).  dcol: Kc*P floats when !plain.
-// implicit: `col` is the conv input x and col^T is gathered inside the GEMM.
+// implicit: `col` is the conv input x, col^T is gathered inside the GEMM, and wpre holds the
+// weight planes (wprep) for the stride-1 data gradient.
 int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *w, const float *div, int Cout,
              float *gx, float *gw, float *dcol, float *part, int64_t part_cap, hipStream_t st, int accum_gx = 0,
-             bool implicit = false) {
-    const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
+             bool implicit = false, const __bf16 *wpre = nullptr) {
+    const int P = g.Ho * g.Wo, kk = g.k * g.k, Kc = g.Cin * kk;
     int rc;
-    if (implicit && !plain_unit(g)) {
-        if (!conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
-        rc = gemm_s3_conv(LdDense<true>{gz, P, Cout}, LdConvWgrad{col, g, Kc, nullptr}, gw, nullptr, div, Cout, Kc, P,
-                          part, part_cap, st);
+    implicit = implicit && !plain_unit(g);
+    if (implicit) {
+        if (!conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
+        rc = gemm_s3_conv(LdDense<true>{gz, P, Cout}, LdWgradTM{col, g.Cin * g.Hs * g.Ws * 4, g, nullptr, 0, 0}, gw,
+                          nullptr, div, Cout, Kc, P, part, part_cap, st);
     } else {
         rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
     }
@@ -232,11 +259,14 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
     if (plain_unit(g)) return gemm(1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st, accum_gx);
     if (!dcol) return LRS_E_WORKSPACE;
     const int Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad);
-    if (implicit && g.stride == 1 && (int64_t)g.Cin * Qp <= (int64_t)Kc * P) {
+    if (implicit && wpre && g.stride == 1 && (int64_t)g.Cin * Qp <= (int64_t)Kc * P) {
         // gxp = W^T (x) gz over the padded domain (implicit, in the dcol space), then fold the
         // padding / upsample
-        rc = gemm_s3_conv(LdWT{w, g.Cin, g.k * g.k}, LdConvDgrad{gz, g, nullptr}, dcol, nullptr, nullptr, g.Cin, Qp,
-                          Cout * g.k * g.k, part, part_cap, st);
+        const int Cop = r16(Cout);
+        const __bf16 *wd = wpre + wprep_fwd_elems(g, Cout);
+        rc = gemm_s3_conv(LdPre{wd, (int64_t)g.Cin * kk * Cop, kk * Cop, g.Cin},
+                          LdDgradTM{gz, Cout * P * 4, g, Cout, Cop, nullptr}, dcol, nullptr, nullptr, g.Cin, Qp,
+                          kk * Cop, part, part_cap, st);
         if (rc) return rc;
         const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
         hipLaunchKernelGGL(k_fold_pad, grid, dim3(256), 0, st, dcol, g, gx, accum_gx);
@@ -388,11 +418,23 @@ extern "C" int64_t lrs_conv2d_col_size(int Cin, int H, int W, int k, int stride,
     return plain_unit(g) ? 0 : (int64_t)Cin * k * k * g.Ho * g.Wo;
 }
 
+// conv workspace: [dcol: Kc*P floats when not plain][split-K partials][weight planes (bf16)]
+struct ConvWs {
+    int64_t dcol, part, wpre_floats;
+};
+inline ConvWs conv_ws(const ConvGeom &g, int Cout) {
+    ConvWs w;
+    w.dcol = plain_unit(g) ? 0 : (int64_t)g.Cin * g.k * g.k * g.Ho * g.Wo;
+    w.part = conv_part_floats(g, Cout);
+    w.wpre_floats = plain_unit(g) ? 0 : (wprep_elems(g, Cout) + 7) / 2;
+    return w;
+}
+
 extern "C" size_t lrs_conv2d_workspace(int Cin, int H, int W, int Cout, int k, int stride, int pad, int upsample) {
     ConvGeom g;
     if (make_geom(Cin, H, W, k, stride, pad, LRS_PAD_ZERO, upsample, g) || Cout <= 0) return 0;
-    const int64_t dcol = plain_unit(g) ? 0 : (int64_t)Cin * k * k * g.Ho * g.Wo;
-    return (size_t)(conv_part_floats(g, Cout) + dcol) * sizeof(float) + 256;
+    const ConvWs w = conv_ws(g, Cout);
+    return (size_t)(w.dcol + w.part + w.wpre_floats) * sizeof(float) + 256;
 }
 
 extern "C" int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const float *w, const float *bias, int Cout,
@@ -402,10 +444,15 @@ extern "C" int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const f
     int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
     if (rc) return rc;
     if (!x || !w || !y || Cout <= 0) return LRS_E_INVALID;
-    if (!col && !plain_unit(g) && !conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
-    const int64_t part = conv_part_floats(g, Cout);
-    if (part > 0 && (!ws || ws_bytes < (size_t)part * sizeof(float))) return LRS_E_WORKSPACE;
-    return conv_fwd(g, x, w, bias, Cout, col, y, (float *)ws, part, (hipStream_t)stream);
+    const bool implicit = !col && !plain_unit(g);
+    if (implicit && !conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
+    const ConvWs cw = conv_ws(g, Cout);
+    const int64_t need = implicit ? cw.dcol + cw.part + cw.wpre_floats : cw.part;
+    if (need > 0 && (!ws || ws_bytes < (size_t)need * sizeof(float))) return LRS_E_WORKSPACE;
+    float *pt = implicit ? (float *)ws + cw.dcol : (float *)ws;
+    __bf16 *wp = implicit ? (__bf16 *)((float *)ws + cw.dcol + cw.part) : nullptr;
+    if (implicit) wprep(g, w, Cout, wp, nullptr, (hipStream_t)stream);
+    return conv_fwd(g, x, w, bias, Cout, col, y, pt, cw.part, (hipStream_t)stream, wp);
 }
 
 extern "C" int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float *w, const float *w_div, int Cin,
@@ -415,12 +462,12 @@ extern "C" int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float
     int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
     if (rc) return rc;
     if (!gy || !col || !w || !gw || Cout <= 0) return LRS_E_INVALID;
-    const int64_t part = conv_part_floats(g, Cout);
-    const int64_t dcol = plain_unit(g) ? 0 : (int64_t)Cin * k * k * g.Ho * g.Wo;
-    if (ws_bytes < (size_t)(part + dcol) * sizeof(float) || (!ws && part + dcol > 0)) return LRS_E_WORKSPACE;
-    float *dc = dcol ? (float *)ws : nullptr;
-    float *pt = (float *)ws + dcol;
-    return conv_bwd(g, gy, col, w, w_div, Cout, gx, gw, dc, pt, part, (hipStream_t)stream);
+    const ConvWs cw = conv_ws(g, Cout);
+    if (ws_bytes < (size_t)(cw.part + cw.dcol) * sizeof(float) || (!ws && cw.part + cw.dcol > 0))
+        return LRS_E_WORKSPACE;
+    float *dc = cw.dcol ? (float *)ws : nullptr;
+    float *pt = (float *)ws + cw.dcol;
+    return conv_bwd(g, gy, col, w, w_div, Cout, gx, gw, dc, pt, cw.part, (hipStream_t)stream);
 }
 
 extern "C" int lrs_conv2d_bwd_x_f32(const float *gy, const float *x, const float *w, const float *w_div, int Cin,
@@ -430,13 +477,15 @@ extern "C" int lrs_conv2d_bwd_x_f32(const float *gy, const float *x, const float
     int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
     if (rc) return rc;
     if (!gy || !x || !w || !gw || Cout <= 0) return LRS_E_INVALID;
-    if (!conv_implicit_ok(g)) return LRS_E_UNSUPPORTED;
-    const int64_t part = conv_part_floats(g, Cout);
-    const int64_t dcol = plain_unit(g) ? 0 : (int64_t)Cin * k * k * g.Ho * g.Wo;
-    if (ws_bytes < (size_t)(part + dcol) * sizeof(float) || (!ws && part + dcol > 0)) return LRS_E_WORKSPACE;
-    float *dc = dcol ? (float *)ws : nullptr;
-    float *pt = (float *)ws + dcol;
-    return conv_bwd(g, gy, x, w, w_div, Cout, gx, gw, dc, pt, part, (hipStream_t)stream, 0, true);
+    if (!conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
+    const ConvWs cw = conv_ws(g, Cout);
+    const int64_t need = cw.dcol + cw.part + cw.wpre_floats;
+    if (ws_bytes < (size_t)need * sizeof(float) || (!ws && need > 0)) return LRS_E_WORKSPACE;
+    float *dc = cw.dcol ? (float *)ws : nullptr;
+    float *pt = (float *)ws + cw.dcol;
+    __bf16 *wp = cw.wpre_floats ? (__bf16 *)((float *)ws + cw.dcol + cw.part) : nullptr;
+    if (wp && gx) wprep(g, w, Cout, wp, wp + wprep_fwd_elems(g, Cout), (hipStream_t)stream);
+    return conv_bwd(g, gy, x, w, w_div, Cout, gx, gw, dc, pt, cw.part, (hipStream_t)stream, 0, true, wp);
 }
 
 extern "C" size_t lrs_bn_act_workspace(int C, int64_t P) {
@@ -582,6 +631,7 @@ struct lrs_dipnet {
         int64_t P = 0, Kc = 0;
         int64_t w_off = -1, b_off = -1, gm_off = -1, bt_off = -1, rs_off = -1;   // params / bn running stats
         int64_t out_off = 0, z_off = -1, col_off = -1, mean_off = -1, istd_off = -1, wn_off = -1, grad_off = 0;
+        int64_t wpre_off = -1;        // implicit convs: bf16 weight planes (wprep)
         int sn_index = -1;            // position in the spectral-norm table
     };
     std::vector<Node> nodes;
@@ -634,8 +684,10 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
             const bool bn = N.d.bn != 0;
             float *z = bn ? net->f(N.z_off) : out;
             const float *w = N.sn_index >= 0 ? net->f(N.wn_off) : net->params + N.w_off;
+            __bf16 *wp = N.wpre_off >= 0 ? (__bf16 *)net->f(N.wpre_off) : nullptr;
+            if (wp) wprep(N.g, w, N.C, wp, N.d.in0 > 0 ? wp + wprep_fwd_elems(N.g, N.C) : nullptr, st);
             rc = conv_fwd(N.g, net->tensor(N.d.in0, x), w, net->params + N.b_off, N.C,
-                          N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st);
+                          N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st, wp);
             if (rc) return rc;
             rc = bn_fwd(z, out, bn ? net->params + N.gm_off : nullptr, bn ? net->params + N.bt_off : nullptr,
                         net->f(N.mean_off), net->f(N.istd_off), bn ? net->bnstats + N.rs_off : nullptr,
@@ -692,7 +744,8 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
             float *gx = t > 0 ? net->f(net->nodes[t - 1].grad_off) : nullptr;
             rc = conv_bwd(N.g, gz, colsrc, w, sn ? net->f(net->scale_off) + N.sn_index : nullptr, N.C, gx,
                           net->grads + N.w_off, !plain_unit(N.g) ? net->f(net->dcol_off) : nullptr,
-                          net->f(net->part_off), net->part_cap, st, t > 0 ? written[t] : 0, N.col_off < 0);
+                          net->f(net->part_off), net->part_cap, st, t > 0 ? written[t] : 0, N.col_off < 0,
+                          N.wpre_off >= 0 ? (const __bf16 *)net->f(N.wpre_off) : nullptr);
             if (rc) return rc;
             if (t > 0) written[t] = 1;
         } else if (N.d.kind == LRS_NODE_BN) {
@@ -790,9 +843,12 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                 if (N.C * N.Kc > net->max_w) net->max_w = N.C * N.Kc;
             }
             if (!plain_unit(N.g)) {
-                if (!(net->implicit && conv_implicit_ok(N.g) && N.P >= implicit_min_pixels())) {
+                if (!(net->implicit && conv_implicit_ok(N.g, N.C) && N.P >= implicit_min_pixels())) {
                     N.col_off = ofs;
                     ofs += align64(N.Kc * N.P);
+                } else {
+                    N.wpre_off = ofs;
+                    ofs += align64((wprep_elems(N.g, N.C) + 1) / 2);
                 }
                 if (N.Kc * N.P > max_dcol) max_dcol = N.Kc * N.P;
             }
