@@ -829,35 +829,46 @@ __global__ __launch_bounds__(256) void k_sn_gram(const SnConv *convs, double *gr
 
 // number of eigenvalues of the symmetric tridiagonal (diag al, squared off-diagonal be2) above x:
 // k minus the sign changes of the characteristic-polynomial sequence p_i = (al_i - x) p_{i-1}
-// - be2_{i-1} p_{i-2} (division-free; rescaled by a power of two every 8 terms)
+// - be2_{i-1} p_{i-2} (division-free; rescaled by a power of two every 4 terms, which changes no
+// sign).  Four terms per block: their eight LDS reads are issued together, off the serial chain.
+// (Measured: holding al / be2 in registers and broadcasting with readlane is slower.)
+__device__ __forceinline__ void sturm_term(double a, double b2, double x, double &p, double &pm, int &changes) {
+    const double pn = __fma_rn(a - x, p, -b2 * pm);
+    // sign change between p_{i-1} and p_i (a zero takes the sign opposite to its predecessor)
+    const bool neg_prev = (p < 0.0) || (p == 0.0 && pm > 0.0);
+    const bool neg_cur = (pn < 0.0) || (pn == 0.0 && !neg_prev);
+    changes += neg_prev != neg_cur;
+    pm = p;
+    p = pn;
+}
+
 __device__ int sturm_gt(const double *al, const double *be2, int k, double x) {
     double pm = 1.0, p = al[0] - x;
     int changes = (p < 0.0) || (p == 0.0);   // p_0 = 1 > 0
-    for (int i = 1; i < k; ++i) {
-        const double pn = __fma_rn(al[i] - x, p, -be2[i - 1] * pm);
-        // sign change between p_{i-1} and p_i (a zero takes the sign opposite to its predecessor)
-        const bool neg_prev = (p < 0.0) || (p == 0.0 && pm > 0.0);
-        const bool neg_cur = (pn < 0.0) || (pn == 0.0 && !neg_prev);
-        changes += neg_prev != neg_cur;
-        pm = p;
-        p = pn;
-        if ((i & 7) == 7) {
-            int e;
-            frexp(fabs(p) > fabs(pm) ? p : pm, &e);
-            p = ldexp(p, -e);
-            pm = ldexp(pm, -e);
-        }
+    int i = 1;
+    for (; i + 4 <= k; i += 4) {
+        const double a0 = al[i], a1 = al[i + 1], a2 = al[i + 2], a3 = al[i + 3];
+        const double b0 = be2[i - 1], b1 = be2[i], b2 = be2[i + 1], b3 = be2[i + 2];
+        sturm_term(a0, b0, x, p, pm, changes);
+        sturm_term(a1, b1, x, p, pm, changes);
+        sturm_term(a2, b2, x, p, pm, changes);
+        sturm_term(a3, b3, x, p, pm, changes);
+        int e;
+        frexp(fabs(p) > fabs(pm) ? p : pm, &e);
+        p = ldexp(p, -e);
+        pm = ldexp(pm, -e);
     }
+    for (; i < k; ++i) sturm_term(al[i], be2[i - 1], x, p, pm, changes);
     return k - changes;
 }
 
 // Largest eigenvalue of the symmetric tridiagonal T_k (diag al, off-diagonal be, be2 = be^2):
-// Gershgorin interval, then `rounds` 256-point multisections (each narrows it 257x).  Whole
-// block; result uniform.
+// the Gershgorin interval (or, with keep, the bracket already in lohi), then `rounds`
+// 256-point multisections (each narrows it 257x).  Whole block; result uniform.
 __device__ double tridiag_max_eig(const double *al, const double *be, const double *be2, int k, int rounds,
-                                  double *lohi, int *best) {
+                                  double *lohi, int *best, bool keep = false) {
     const int t = threadIdx.x;
-    if (t == 0) {
+    if (t == 0 && !keep) {
         double lo = 1e300, hi = -1e300;
         for (int i = 0; i < k; ++i) {
             const double r = (i > 0 ? be[i - 1] : 0.0) + (i + 1 < k ? be[i] : 0.0);
@@ -922,12 +933,15 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     // two-value reduction (||r_k||^2, r_k.u'), then beta_k = ||r_k||, q_k = r_k / beta_k,
     // alpha_k = r_k.u' / beta_k^2 and r_{k+1} = u'/beta_k - alpha_k q_k - beta_k q_{k-1}.
     // Two barriers per step.
+    // (Measured: warm-starting from the previous step's top Ritz vector does not shorten the
+    // iteration: with Adam at lr 0.1 the weights change by O(their size) every step.)
     double rr = (row < m) ? 1.0 + 0.5 * sin(0.7 * (double)row + 0.3) : 0.0;
     double qprev = 0.0, theta_prev = -1.0;
     __shared__ double red2[2][8];
     if (half == 0) q[row] = rr;
     __syncthreads();
     int k = 0;
+    bool converged = false;
     for (; k < m; ++k) {
         double acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};    // 8 independent FMA chains
 #pragma unroll
@@ -961,14 +975,16 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
             const double th = tridiag_max_eig(al, be, be2, k + 1, 4, lohi, &best_s);
             const bool conv = fabs(th - theta_prev) <= 1e-11 * th;
             theta_prev = th;
-            if (conv) { ++k; break; }
+            if (conv) { ++k; converged = true; break; }
         }
         if (half == 0) q[row] = rr;                   // the matvec reads of q finished before the barrier
         __syncthreads();
     }
     __syncthreads();
     if (prof && t == 0) { prof[blockIdx.x * 8 + 2] = wall_clock64(); prof[blockIdx.x * 8 + 4] = k; }
-    const double lmax = m > 0 ? tridiag_max_eig(al, be, be2, k, 8, lohi, &best_s) : 0.0;
+    // converged at a check: T_k is the matrix that check bracketed (4 rounds); 2 more rounds
+    // give the same 1e-15 width as 8 rounds from the Gershgorin interval
+    const double lmax = m > 0 ? tridiag_max_eig(al, be, be2, k, converged ? 2 : 8, lohi, &best_s, converged) : 0.0;
     if (prof && t == 0) prof[blockIdx.x * 8 + 3] = wall_clock64();
     if (t == 0) {
         const float s32 = (float)sqrt(fmax(lmax, 0.0));
