@@ -901,9 +901,10 @@ __device__ double tridiag_max_eig(const double *al, const double *be, const doub
 
 // One workgroup (256 threads) per conv: Lanczos (no reorthogonalisation: the extreme Ritz value
 // converges regardless, Paige) with the Gram in registers (thread t holds half a row, 64
-// doubles).  Every 8 steps from step 16 the largest Ritz value is located to ~1e-10 (4
+// doubles).  Every 8 steps from step 24 the largest Ritz value is located to ~1e-10 (4
 // multisection rounds); the iteration stops when it moved less than 1e-11 relative (typically
-// 30-40 steps for these weights instead of m = 128), then 8 rounds pin lambda_max.
+// 30-40 steps for these weights instead of m = 128), then 2 more rounds from that check's bracket
+// (8 from Gershgorin if no check converged) pin lambda_max.
 // sigma32 = float(sqrt(lambda_max)); scale = max(1, sigma32 / ln_lambda) (float32, as torch).
 __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const double *gram, float *sigma,
                                                   float *scale, float ln_lambda, long long *prof) {
