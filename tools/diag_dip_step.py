@@ -19,7 +19,7 @@ def nodes_for(net, C):
 
 
 for net, C, H, W in CASES:
-    for prec in (0, 1):
+    for prec in ((1,) if os.environ.get('DIAG_B3_ONLY') else (0, 1)):
         L.lrs_dip_set_precision(prec)
         n = DipNet(nodes_for(net, C), C, H, W)
         n.init_params(1)
@@ -28,14 +28,16 @@ for net, C, H, W in CASES:
         t = torch.rand(n.out_shape, device="cuda", generator=g)
         m = (torch.rand(n.out_shape[1:], device="cuda", generator=g) > 0.2).float()
         steps = 20 if H <= 200 else 5
-        n.train_steps(x, t, m, 2)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        n.train_steps(x, t, m, steps)
-        e1.record()
-        torch.cuda.synchronize()
-        print(f"{net:9s} {C}x{H}x{W} precision {'split-bf16 implicit' if prec else 'f32 explicit    '}: "
-              f"{e0.elapsed_time(e1) / steps:8.3f} ms/step  loss {n.last_loss():.6e}", flush=True)
+        for graph in (False, True):
+            n.train_steps(x, t, m, 2, use_graph=graph)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            n.train_steps(x, t, m, steps, use_graph=graph)
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"{net:9s} {C}x{H}x{W} precision {'split-bf16 implicit' if prec else 'f32 explicit    '} "
+                  f"{'graph' if graph else 'eager'}: {e0.elapsed_time(e1) / steps:8.3f} ms/step  "
+                  f"loss {n.last_loss():.6e}", flush=True)
         del n
 L.lrs_dip_set_precision(1)
