@@ -616,14 +616,14 @@ struct BnArgs {
     int lip;                     // BatchNormSpectralNorm rescale (1-Lip) or plain BatchNorm2d
 };
 
-// partial sums of (z - K), (z - K)^2 over this workgroup's slice, K = z[c][0] (stable variance)
-__global__ __launch_bounds__(kBnThreads) void k_bn_stats(BnArgs a) {
-    __shared__ double red[2 * kBnThreads / 64];
-    const int c = blockIdx.y, sb = blockIdx.x;
+// partial sums of (z - K), (z - K)^2 over this workgroup's slice, K = z[c][0] (stable variance);
+// block-reduced (valid in every thread)
+__device__ __forceinline__ void bn_stats_body(const BnArgs &a, int c, int sb, double &s1, double &s2, double *red) {
     const float *z = a.z + (int64_t)c * a.P;
     const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
     const double K = (double)z[0];
-    double s1 = 0.0, s2 = 0.0;
+    s1 = 0.0;
+    s2 = 0.0;
     for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const double d = (double)z[i] - K;
         s1 += d;
@@ -632,6 +632,13 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_stats(BnArgs a) {
     int par = 0;
     s1 = block_sum_d1(s1, red, par);
     s2 = block_sum_d1(s2, red, par);
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_bn_stats(BnArgs a) {
+    __shared__ double red[2 * kBnThreads / 64];
+    const int c = blockIdx.y, sb = blockIdx.x;
+    double s1, s2;
+    bn_stats_body(a, c, sb, s1, s2, red);
     if (threadIdx.x == 0) {
         double *pp = a.part + ((int64_t)c * a.S + sb) * 3;
         pp[0] = s1;
@@ -639,24 +646,16 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_stats(BnArgs a) {
     }
 }
 
-// every workgroup reduces its channel's partials (fixed order), then normalises its slice
-__global__ __launch_bounds__(kBnThreads) void k_bn_apply(BnArgs a) {
-    __shared__ float redf[kBnThreads / 64];
-    __shared__ float st_s[2];
-    const int c = blockIdx.y, sb = blockIdx.x;
+// normalise + affine + activation of this workgroup's slice; t1, t2 = the channel's summed
+// partials (read by thread 0 only)
+__device__ __forceinline__ void bn_apply_body(const BnArgs &a, int c, int sb, double t1, double t2, float *redf,
+                                              float *st_s) {
     const int64_t off = (int64_t)c * a.P;
     const float *z = a.z + off;
     float *y = a.y + off;
     const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
-    if (!a.bn) {
-        for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) y[i] = act_fwd(z[i], a.act);
-        return;
-    }
     const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
     if (threadIdx.x == 0) {
-        double t1 = 0.0, t2 = 0.0;
-        const double *q = a.part + (int64_t)c * a.S * 3;
-        for (int j = 0; j < a.S; ++j) { t1 += q[3 * j]; t2 += q[3 * j + 1]; }
         const double m = t1 / a.P;
         double var = t2 / a.P - m * m;
         if (var < 0.0) var = 0.0;
@@ -680,6 +679,36 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_apply(BnArgs a) {
     for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) y[i] = act_fwd((z[i] - m32) * is32 * gm + bt, a.act);
 }
 
+__global__ __launch_bounds__(kBnThreads) void k_bn_apply(BnArgs a) {
+    __shared__ float redf[kBnThreads / 64];
+    __shared__ float st_s[2];
+    const int c = blockIdx.y, sb = blockIdx.x;
+    if (!a.bn) {
+        const int64_t off = (int64_t)c * a.P;
+        const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
+        for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) a.y[off + i] = act_fwd(a.z[off + i], a.act);
+        return;
+    }
+    double t1 = 0.0, t2 = 0.0;
+    if (threadIdx.x == 0) {
+        const double *q = a.part + (int64_t)c * a.S * 3;
+        for (int j = 0; j < a.S; ++j) { t1 += q[3 * j]; t2 += q[3 * j + 1]; }
+    }
+    bn_apply_body(a, c, sb, t1, t2, redf, st_s);
+}
+
+// S == 1 (a channel fits one workgroup): statistics and apply in one launch, the same
+// arithmetic as k_bn_stats + k_bn_apply (0 + the single partial)
+__global__ __launch_bounds__(kBnThreads) void k_bn_fwd1(BnArgs a) {
+    __shared__ double red[2 * kBnThreads / 64];
+    __shared__ float redf[kBnThreads / 64];
+    __shared__ float st_s[2];
+    const int c = blockIdx.y;
+    double s1, s2;
+    bn_stats_body(a, c, 0, s1, s2, red);
+    bn_apply_body(a, c, 0, 0.0 + s1, 0.0 + s2, redf, st_s);
+}
+
 struct BnBwdArgs {
     const float *gy;             // [C][P] dL/dy
     const float *y, *z;          // activation output, conv output
@@ -694,9 +723,7 @@ struct BnBwdArgs {
     int accum;                   // gz += instead of gz =
 };
 
-__global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
-    __shared__ double red[2 * kBnThreads / 64];
-    const int c = blockIdx.y, sb = blockIdx.x;
+__device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int sb, double (&o)[3], double *red) {
     const int64_t off = (int64_t)c * a.P;
     const float *gy = a.gy + off, *y = a.y + off, *z = a.z + off;
     const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
@@ -714,31 +741,31 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
         for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) sg += (double)act_bwd(gy[i], y[i], a.act);
     }
     int par = 0;
-    sg = block_sum_d1(sg, red, par);
-    sgx = block_sum_d1(sgx, red, par);
-    sx = block_sum_d1(sx, red, par);
+    o[0] = block_sum_d1(sg, red, par);
+    o[1] = block_sum_d1(sgx, red, par);
+    o[2] = block_sum_d1(sx, red, par);
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
+    __shared__ double red[2 * kBnThreads / 64];
+    const int c = blockIdx.y, sb = blockIdx.x;
+    double o[3];
+    bn_bwd_stats_body(a, c, sb, o, red);
     if (threadIdx.x == 0) {
         double *pp = a.part + ((int64_t)c * a.S + sb) * 3;
-        pp[0] = sg;
-        pp[1] = sgx;
-        pp[2] = sx;
+        pp[0] = o[0];
+        pp[1] = o[1];
+        pp[2] = o[2];
     }
 }
 
-__global__ __launch_bounds__(kBnThreads) void k_bn_bwd_apply(BnBwdArgs a) {
-    __shared__ float redf[kBnThreads / 64];
-    __shared__ float st_s[2];
-    const int c = blockIdx.y, sb = blockIdx.x;
+// t = the channel's summed partials (read by thread 0 only)
+__device__ __forceinline__ void bn_bwd_apply_body(const BnBwdArgs &a, int c, int sb, const double (&t)[3],
+                                                  float *redf, float *st_s) {
     const int64_t off = (int64_t)c * a.P;
     const float *gy = a.gy + off, *y = a.y + off, *z = a.z + off;
     float *gz = a.gz + off;
     const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
-    double t[3] = {0.0, 0.0, 0.0};
-    if (threadIdx.x == 0 && (a.bn || (sb == 0 && a.gbias))) {
-        const double *q = a.part + (int64_t)c * a.S * 3;
-        for (int j = 0; j < a.S; ++j)
-            for (int e = 0; e < 3; ++e) t[e] += q[3 * j + e];
-    }
     if (!a.bn) {
         if (threadIdx.x == 0 && sb == 0 && a.gbias) a.gbias[c] = (float)t[0];
         for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
@@ -770,6 +797,31 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_apply(BnBwdArgs a) {
         const float v = k * (g - mg - xh * mgx);
         gz[i] = a.accum ? gz[i] + v : v;
     }
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_bn_bwd_apply(BnBwdArgs a) {
+    __shared__ float redf[kBnThreads / 64];
+    __shared__ float st_s[2];
+    const int c = blockIdx.y, sb = blockIdx.x;
+    double t[3] = {0.0, 0.0, 0.0};
+    if (threadIdx.x == 0 && (a.bn || (sb == 0 && a.gbias))) {
+        const double *q = a.part + (int64_t)c * a.S * 3;
+        for (int j = 0; j < a.S; ++j)
+            for (int e = 0; e < 3; ++e) t[e] += q[3 * j + e];
+    }
+    bn_bwd_apply_body(a, c, sb, t, redf, st_s);
+}
+
+// S == 1: statistics and apply in one launch (same arithmetic as the two-kernel path)
+__global__ __launch_bounds__(kBnThreads) void k_bn_bwd1(BnBwdArgs a) {
+    __shared__ double red[2 * kBnThreads / 64];
+    __shared__ float redf[kBnThreads / 64];
+    __shared__ float st_s[2];
+    const int c = blockIdx.y;
+    double o[3];
+    bn_bwd_stats_body(a, c, 0, o, red);
+    const double t[3] = {0.0 + o[0], 0.0 + o[1], 0.0 + o[2]};
+    bn_bwd_apply_body(a, c, 0, t, redf, st_s);
 }
 
 // ------------------------------------------------------------------------------------------

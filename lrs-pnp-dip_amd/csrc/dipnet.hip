@@ -301,8 +301,12 @@ int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, floa
     const int S = bn_split(P);
     const int chunk = (int)((P + S - 1) / S);
     BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, part, C, (int)P, S, chunk, gamma ? 1 : 0, act, eps, mom, lip};
-    if (gamma) hipLaunchKernelGGL(k_bn_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
-    hipLaunchKernelGGL(k_bn_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
+    if (gamma && S == 1) {
+        hipLaunchKernelGGL(k_bn_fwd1, dim3(1, C), dim3(kBnThreads), 0, st, a);
+    } else {
+        if (gamma) hipLaunchKernelGGL(k_bn_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
+        hipLaunchKernelGGL(k_bn_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
+    }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -314,8 +318,12 @@ int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, 
     const int chunk = (int)((P + S - 1) / S);
     BnBwdArgs a{gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, part, C, (int)P, S, chunk,
                 gamma ? 1 : 0, act, lip, accum};
-    if (gamma || gbias) hipLaunchKernelGGL(k_bn_bwd_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
-    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
+    if ((gamma || gbias) && S == 1) {
+        hipLaunchKernelGGL(k_bn_bwd1, dim3(1, C), dim3(kBnThreads), 0, st, a);
+    } else {
+        if (gamma || gbias) hipLaunchKernelGGL(k_bn_bwd_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
+        hipLaunchKernelGGL(k_bn_bwd_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
+    }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
