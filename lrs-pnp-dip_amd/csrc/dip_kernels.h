@@ -1084,11 +1084,16 @@ __global__ void k_masked_mse(const float *__restrict__ out, const float *__restr
 __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
                        float *__restrict__ v, int64_t n, const int *step, float lr, float b1, float b2,
                        float eps) {
-    const int t = *step;
-    const double bc1 = 1.0 - pow((double)b1, (double)t);
-    const double bc2 = 1.0 - pow((double)b2, (double)t);
-    const float step_size = (float)((double)lr / bc1);
-    const float bc2s = (float)sqrt(bc2);
+    __shared__ float sc[2];   // the bias corrections, once per workgroup (fp64 pow is costly)
+    if (threadIdx.x == 0) {
+        const int t = *step;
+        const double bc1 = 1.0 - pow((double)b1, (double)t);
+        const double bc2 = 1.0 - pow((double)b2, (double)t);
+        sc[0] = (float)((double)lr / bc1);
+        sc[1] = (float)sqrt(bc2);
+    }
+    __syncthreads();
+    const float step_size = sc[0], bc2s = sc[1];
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float gi = g[i];
         const float mi = m[i] + (1.0f - b1) * (gi - m[i]);          // exp_avg.lerp_(grad, 1-b1)
