@@ -336,8 +336,17 @@ template <class LA, class LB>
 __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
     __shared__ __attribute__((aligned(16))) S3Tile As, Bs;
     __shared__ __attribute__((aligned(16))) int tab[kS3TabInts];
-    const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 128;
-    const int kbeg = blockIdx.z * g.kchunk;
+    // XCD-aware tile order: the hardware deals workgroup L to XCD L % 8 (placement matters for
+    // speed only), so consecutive logical tiles -- neighbouring pixel tiles that share input rows,
+    // the N-tiles of one split-K chunk that share its A rows -- are given to one XCD and meet in
+    // its L2 instead of being fetched from HBM by all eight
+    const int T = gridDim.x * gridDim.y * gridDim.z;
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = L & 7, q8 = T >> 3, r8 = T & 7;
+    const int j = xcd * q8 + min(xcd, r8) + (L >> 3);
+    const int bx = j % gridDim.x, byz = j / gridDim.x, by = byz % gridDim.y, bz = byz / gridDim.y;
+    const int m0 = by * 128, n0 = bx * 128;
+    const int kbeg = bz * g.kchunk;
     const int kend = min(g.K, kbeg + g.kchunk);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
@@ -387,7 +396,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
         }
         __syncthreads();
     }
-    float *C = g.C + (int64_t)blockIdx.z * g.M * g.N;
+    float *C = g.C + (int64_t)bz * g.M * g.N;
     const bool final_out = gridDim.z == 1;
     const float dv = (final_out && g.div) ? *g.div : 1.0f;
 #pragma unroll
