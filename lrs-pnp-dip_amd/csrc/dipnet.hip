@@ -961,15 +961,7 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     net->misc_off_bytes = (int64_t)bytes;
     bytes += 256;
     net->ws_bytes = bytes;
-    hipError_t e = hipStreamCreateWithFlags(&net->side, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming);
-    net->ev_fork.assign(net->nodes.size(), nullptr);
-    for (size_t i = 0; i < net->nodes.size() && e == hipSuccess; ++i)
-        e = hipEventCreateWithFlags(&net->ev_fork[i], hipEventDisableTiming);
-    if (e != hipSuccess) {
-        lrs_dipnet_destroy(net);
-        return (int)e;
-    }
+    net->ev_fork.assign(net->nodes.size(), nullptr);   // side stream + events: ensure_side()
     *out = net;
     return LRS_OK;
 }
@@ -1086,11 +1078,23 @@ extern "C" const float *lrs_dipnet_output(const lrs_dipnet *net) {
 
 extern "C" const float *lrs_dipnet_grads(const lrs_dipnet *net) { return net ? net->grads : nullptr; }
 
+// The side stream and its fork/join events are created on the first training call (outside any
+// capture), so that creating a net and querying its layout needs no device.
+static int ensure_side(lrs_dipnet *net) {
+    if (!net->fork_w || net->side) return LRS_OK;
+    hipError_t e = hipStreamCreateWithFlags(&net->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming);
+    for (size_t i = 0; i < net->ev_fork.size() && e == hipSuccess; ++i)
+        e = hipEventCreateWithFlags(&net->ev_fork[i], hipEventDisableTiming);
+    return (int)e;
+}
+
 extern "C" int lrs_dipnet_train_steps(lrs_dipnet *net, const float *x, const float *target, const float *mask,
                                       float lr, float beta1, float beta2, float eps, lrs_es_state *es, float *ring,
                                       int nsteps, int use_graph, void *stream) {
     if (!net || !net->ws || !x || !target || nsteps < 0 || (es && !ring)) return LRS_E_INVALID;
     hipStream_t st = (hipStream_t)stream;
+    if (const int rs = ensure_side(net)) return rs;
     if (!use_graph) {
         for (int s = 0; s < nsteps; ++s) {
             const int rc = dipnet_step(net, x, target, mask, lr, beta1, beta2, eps, es, ring, st);
