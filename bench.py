@@ -9,7 +9,9 @@ Inputs are resident in HBM before the timed region.
 
 Multi-GPU (torchrun): one independent cube per rank (seed = rank), no data-path collective
 (weak scaling, SURVEY.md §8e); barrier + synchronize around the K timed steps, MAX over ranks;
-value = (ranks * K) / max_time.
+value = (ranks * K) / max_time.  With --split-cube: ONE cube (seed 0) in pixel-row slabs, one per
+rank, with an fp64 all-reduce of the B x B SVT Gram per iteration (strong scaling, value =
+K / max_time; lrspnp.dist.slab_solver).
 
 Rank 0 prints one JSON line, including
   roofline    : the dominant kernel (lrs_ista_f32 / k_ista_b3) — algorithmic fp32-GEMM FLOPs per
@@ -51,6 +53,8 @@ def parse():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split-cube", action="store_true",
+                    help="one cube over all ranks in pixel-row slabs (strong scaling; SVT Gram all-reduce)")
     ap.add_argument("--workload", default="pnp", choices=["pnp", "dip", "dip-pro"],
                     help="pnp: BASELINE configs[1] (the headline); dip: configs[2], LRS-PnP-DIP(1-Lip) on a "
                          "196x196x198 cube (the 200x200 cube cropped to a size the U-Net maps onto itself); "
@@ -197,14 +201,26 @@ def main():
     from lrspnp.metrics import mpsnr
 
     H, W, B = (int(v) for v in args.cube.split("x"))
-    Y, M, Dct, clean = make_problem(H, W, B, args.bb, args.K, seed=ctx.rank)   # one cube per rank
+    split = args.split_cube
+    # one cube per rank (seed = rank), or with --split-cube one cube (seed 0) in row slabs
+    Y, M, Dct, clean = make_problem(H, W, B, args.bb, args.K, seed=0 if split else ctx.rank)
     cfg = LrsPnPConfig(bb=args.bb, sliding=args.bb, Nit=args.nit, variant="spec2")
     t0 = time.perf_counter()
-    s = LrsPnP(Y, M, Dct, cfg)
+    if split:
+        s, _ = D.slab_solver(Y, M, Dct, cfg, ctx)
+    else:
+        s = LrsPnP(Y, M, Dct, cfg)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
     clean_d = torch.from_numpy(clean).cuda()
-    mp0 = mpsnr(s.X, clean_d)
+
+    def cube_mpsnr():
+        if not split:
+            return mpsnr(s.X, clean_d)
+        X = D.gather_rows(s.X, ctx)
+        return mpsnr(torch.from_numpy(X).cuda(), clean_d) if X is not None else float("nan")
+
+    mp0 = cube_mpsnr()
 
     # dominant-kernel timing: HIP events on the stream the ISTA kernel is launched on
     ev = []
@@ -234,7 +250,7 @@ def main():
     elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
     ops.ista = orig_ista
     ista_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    mp1 = mpsnr(s.X, clean_d)
+    mp1 = cube_mpsnr()
     world, rank = ctx.world, ctx.rank
     mps = D.gather_scalars([mp0, mp1], ctx)
 
@@ -250,20 +266,22 @@ def main():
             traffic = None
     out = {
         "metric": METRIC,
-        "value": world * args.steps / elapsed,
+        "value": (1 if split else world) * args.steps / elapsed,
         "unit": "outer_iters/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if split else "weak",
         "vs_baseline": None,
         "dtype": "f32 (MFMA) + f64 (NLM prox, Gram/eig)",
         "data": "synthetic (seeded low-rank cube per rank, tiled low_rank_sparsity_mask, seeded K=256 dictionary)",
         "config": {"workload": f"LRS-PnP (no DIP) {args.cube} cube, {args.bb}x{args.bb} blocks, K={K}, "
                                f"Nit={args.nit} inner ISTA, SVT low-rank prox (BASELINE configs[1])",
-                   "blocks": nb, "parallelism": f"{world} independent cube(s), one per GPU"},
+                   "blocks": int(ops.block_grid(Y.shape[0], B, args.bb, args.bb)[0].size),
+                   "parallelism": (f"1 cube in {world} pixel-row slab(s), fp64 Gram all-reduce per iteration"
+                                   if split else f"{world} independent cube(s), one per GPU")},
         "roofline": {"bound": "mfma", "kernel": "k_ista_ln2 (lrs_ista_f32)", "achieved": achieved,
                      "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                      "traffic": traffic, "flops_per_launch": flops, "ms_per_launch": ista_ms},

@@ -133,6 +133,13 @@ int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64_t P, int64
                      void *ws, size_t ws_bytes, void *stream);
 int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau,
                        float *U, double *s_out, int warm, void *ws, size_t ws_bytes, void *stream);
+/* Byte offset and leading dimension (Bp = B rounded up to even) of the fp64 Gram (X + c2 L2)^T
+ * (X + c2 L2) that lrs_svt_gram_f32 leaves in ws. A caller that holds one row slab of the
+ * unfolded cube per rank sums the slabs' Grams in place (all-reduce of Bp*Bp doubles) between
+ * _gram and _finish: the Gram is additive over pixel rows (single cube on
+ * several GPUs). Not valid with LRS_SVT_JACOBI | LRS_SVT_WARM (its warm-start products are
+ * formed from the local Gram inside _gram). Host-only, no device access. */
+int lrs_svt_gram_offset(int64_t P, int64_t B, int64_t *offset_bytes, int64_t *ld);
 
 /* ---- col2im + closed-form X update + dual updates ------------------------------------------
  * IMout = sum over covering blocks (block order) of phi, Weight = count, lambda1_sum = repeated

@@ -686,6 +686,15 @@ extern "C" size_t lrs_svt_workspace(int64_t P, int64_t B) {
     return svt_ws_bytes(P, B);
 }
 
+extern "C" int lrs_svt_gram_offset(int64_t P, int64_t B, int64_t *offset_bytes, int64_t *ld) {
+    if (P <= 0 || B <= 0 || !offset_bytes || !ld) return LRS_E_INVALID;
+    if (B + (B & 1) > kMaxBp) return LRS_E_UNSUPPORTED;
+    const SvtWs w = svt_ws_layout(nullptr, P, B);
+    *offset_bytes = (int64_t)((char *)w.G - (char *)nullptr);
+    *ld = w.Bp;
+    return LRS_OK;
+}
+
 // Stage 1 (multi-workgroup): fp64 Gram on the matrix cores and, for a warm Jacobi, A0 = V^T G V.
 extern "C" int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, int warm, void *ws,
                                 size_t ws_bytes, void *stream) {

@@ -63,6 +63,7 @@ def _declare(L):
         "lrs_svt_f32": (i32, [vp, vp, f32, i64, i64, f64, vp, vp, i32, vp, sz, vp]),
         "lrs_svt_gram_f32": (i32, [vp, vp, f32, i64, i64, i32, vp, sz, vp]),
         "lrs_svt_finish_f32": (i32, [vp, vp, f32, i64, i64, f64, vp, vp, i32, vp, sz, vp]),
+        "lrs_svt_gram_offset": (i32, [i64, i64, vp, vp]),
         "lrs_diag_svt_state": (i32, [vp, i64, i64, vp]),
         "lrs_admm_update_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, i64, vp, vp,
                                       vp, vp, f32, f32, f32, vp, vp, vp]),

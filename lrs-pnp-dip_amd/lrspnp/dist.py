@@ -86,3 +86,77 @@ def gather_scalars(values: list[float], ctx: Ctx) -> list[list[float]] | None:
     out = [None] * ctx.world
     dist.all_gather_object(out, list(values))
     return out if ctx.rank == 0 else None
+
+
+# ---- one cube over several ranks: pixel-row slabs (SURVEY.md §8e, "single cube") -----------------
+#
+# The unfolded cube X (P x B, p = i + H j) is cut into row slabs aligned to the block size. With
+# slidingDis == bb (every reference main: main_LRS_PnP.py:237-238) the blocks of a slab are exactly
+# the cube's blocks over those rows (get_image_block, main_LRS_PnP.py:73-107: the extra block row
+# at P - bb when bb does not divide P belongs to the last slab), so the sparse coding, col2im and
+# X / dual updates are slab-local. The only coupled step is the SVT: its Gram is the sum of the
+# slabs' Grams (B x B fp64, one all-reduce per outer iteration), after which every rank runs the
+# same eigensolver and applies U = Z (I - E) to its own rows.
+
+
+def slab_rows(P: int, bb: int, rank: int, world: int) -> tuple[int, int]:
+    """[p0, p1) of rank's slab: whole block rows of bb pixels, split as evenly as possible; the
+    last slab also takes the P % bb tail rows (whose appended block starts at P - bb)."""
+    nfull = P // bb
+    if nfull < world:
+        raise ValueError(f"{P} rows in blocks of {bb} give {nfull} block rows, fewer than {world} ranks")
+    base, extra = divmod(nfull, world)
+    r0 = rank * base + min(rank, extra)
+    r1 = r0 + base + (1 if rank < extra else 0)
+    return r0 * bb, (P if rank == world - 1 else r1 * bb)
+
+
+class SlabComm:
+    """Sum-all-reduce of device tensors for a row-slab shard, stream-ordered.
+
+    nccl (RCCL over xGMI on the box): the collective is enqueued behind `stream`'s work and
+    later work on `stream` waits for it; the host does not block. gloo (CPU tests, or several
+    ranks sharing one GPU): the tensor is staged through host memory after `stream` drains."""
+
+    def __init__(self, ctx: Ctx):
+        self.ctx = ctx
+
+    def allreduce_(self, t: torch.Tensor, stream) -> None:
+        if not self.ctx.distributed:
+            return
+        if dist.get_backend() == "nccl":
+            with torch.cuda.stream(stream):
+                dist.all_reduce(t)
+            return
+        if t.is_cuda:
+            stream.synchronize()
+            h = t.cpu()
+            dist.all_reduce(h)
+            with torch.cuda.stream(stream):
+                t.copy_(h)
+        else:
+            dist.all_reduce(t)
+
+
+def slab_solver(Y, M, D, cfg, ctx: Ctx, device="cuda"):
+    """This rank's LrsPnP over its row slab of the whole-cube inputs Y, M (P x B, host arrays);
+    returns (solver, (p0, p1))."""
+    from .solver import LrsPnP
+    if cfg.sliding != cfg.bb:
+        raise ValueError("row-slab sharding needs slidingDis == bb")
+    P = Y.shape[0]
+    p0, p1 = slab_rows(P, cfg.bb, ctx.rank, ctx.world)
+    comm = SlabComm(ctx) if ctx.distributed else None
+    return LrsPnP(Y[p0:p1], M[p0:p1], D, cfg, device=device, comm=comm), (p0, p1)
+
+
+def gather_rows(X: torch.Tensor, ctx: Ctx):
+    """The whole unfolded matrix from the ranks' row slabs, on rank 0 (numpy; None elsewhere).
+    Outside any timed region (object gather through host memory)."""
+    x = X.detach().cpu().numpy()
+    if not ctx.distributed:
+        return x
+    import numpy as np
+    out = [None] * ctx.world
+    dist.all_gather_object(out, x)
+    return np.concatenate(out, axis=0) if ctx.rank == 0 else None

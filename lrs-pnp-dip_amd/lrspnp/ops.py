@@ -14,7 +14,7 @@ from ._lib import (ALPHA_FRO4, ALPHA_SOFT, ALPHA_SPEC2, PROX_NLM, PROX_NLM_MATLA
                    device_lib, lib)
 
 __all__ = ["nlm_col", "block_grid", "cover_ranges", "im2col", "ista_alpha", "ista", "svt_workspace",
-           "svt", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT",
+           "svt", "svt_gram", "svt_gram_view", "svt_finish", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT",
            "PROX_NLM_MATLAB"]
 
 
@@ -172,6 +172,15 @@ def svt_gram(X, L2, c2: float, ws, warm=False, stream=None, method="tri"):
     P, B = X.shape
     check(L.lrs_svt_gram_f32(_p(X), _p(L2), float(c2), P, B, _svt_flags(warm, method), _p(ws), ws.numel(),
                              _s(stream)), "lrs_svt_gram_f32")
+
+
+def svt_gram_view(ws, P: int, B: int) -> torch.Tensor:
+    """The fp64 Gram (Bp x Bp, Bp = B rounded up to even) that svt_gram() leaves in `ws`, as a
+    tensor view: a slab-sharded caller all-reduces it in place before svt_finish()."""
+    off, ld = ctypes.c_int64(), ctypes.c_int64()
+    check(lib().lrs_svt_gram_offset(P, B, ctypes.byref(off), ctypes.byref(ld)), "lrs_svt_gram_offset")
+    n = ld.value * ld.value
+    return ws[off.value: off.value + 8 * n].view(torch.float64).view(ld.value, ld.value)
 
 
 def svt_finish(X, L2, c2: float, tau: float, ws, U, s_out=None, warm=False, stream=None, method="tri"):

@@ -72,8 +72,11 @@ class LrsPnP:
     dictionary with n = bb*bb.  All float32 (numpy or torch); copied to the device once.
     """
 
-    def __init__(self, Y, M, D, cfg: LrsPnPConfig | None = None, device="cuda", image_shape=None):
+    def __init__(self, Y, M, D, cfg: LrsPnPConfig | None = None, device="cuda", image_shape=None, comm=None):
         self.cfg = cfg = cfg or LrsPnPConfig()
+        # comm: None (whole cube here) or a row-slab communicator (lrspnp.dist.SlabComm): Y, M are
+        # then this rank's pixel-row slab and the SVT Gram / convergence sums are all-reduced
+        self.comm = comm
         dev = torch.device(device)
         f = lambda a: torch.as_tensor(np.asarray(a, np.float32) if not isinstance(a, torch.Tensor) else a,
                                       dtype=torch.float32).to(dev).contiguous()
@@ -131,8 +134,11 @@ class LrsPnP:
         self.lowrank_stream = torch.cuda.Stream(device=dev)
         self.iteration = 0
         self.dip = None
+        if comm is not None and (cfg.lowrank != "svt" or cfg.svt_method != "tri"):
+            raise LrsError("a row-slab shard needs lowrank='svt' with svt_method='tri'")
         if cfg.lowrank == "svt":
             self.svt_ws = ops.svt_workspace(self.P, self.B, dev)
+            self.gram = ops.svt_gram_view(self.svt_ws, self.P, self.B) if comm is not None else None
         elif cfg.lowrank == "dip":
             self._init_dip(image_shape, dev)
         else:
@@ -189,6 +195,8 @@ class LrsPnP:
         lr.wait_stream(main)
         # low-rank prox, first half (whole chip, ~0.2 ms): fp64 Gram (+ Jacobi warm-start products)
         ops.svt_gram(self.X, self.L2, self.c2, self.svt_ws, warm=warm, stream=lr, method=self.cfg.svt_method)
+        if self.comm is not None:
+            self.comm.allreduce_(self.gram, lr)       # the cube's Gram = sum of the slabs' Grams
         gram_done = lr.record_event()
         # second half: the one-workgroup eigensolver then runs beside the sparse coding
         ops.svt_finish(self.X, self.L2, self.c2, self.tau, self.svt_ws, self.U, warm=warm, stream=lr,
@@ -224,4 +232,8 @@ class LrsPnP:
 
     def convergence(self):
         """state_convergence (main_LRS_PnP.py:23-25) of X, lambda_1, lambda_2 for the last step."""
-        return torch.log(torch.sqrt(self.norms)).cpu().tolist()
+        norms = self.norms
+        if self.comm is not None:
+            norms = norms.clone()
+            self.comm.allreduce_(norms, torch.cuda.current_stream())
+        return torch.log(torch.sqrt(norms)).cpu().tolist()
