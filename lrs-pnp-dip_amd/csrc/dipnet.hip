@@ -296,11 +296,16 @@ inline int bn_split(int64_t P) {
 
 inline int64_t bn_part_doubles(int C, int64_t P) { return (int64_t)C * bn_split(P) * 3; }
 
+inline bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
 int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, float *mean, float *invstd, float *rm,
            float *rv, int C, int64_t P, int act, float eps, float mom, double *part, hipStream_t st, int lip = 1) {
     const int S = bn_split(P);
-    const int chunk = (int)((P + S - 1) / S);
-    BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, part, C, (int)P, S, chunk, gamma ? 1 : 0, act, eps, mom, lip};
+    const int vec = (P % 4 == 0 && al16(z) && al16(y)) ? 1 : 0;
+    int chunk = (int)((P + S - 1) / S);
+    if (vec) chunk = (chunk + 3) & ~3;
+    BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, part, C, (int)P, S, chunk, gamma ? 1 : 0, act, eps, mom, lip,
+             vec};
     if (gamma && S == 1) {
         hipLaunchKernelGGL(k_bn_fwd1, dim3(1, C), dim3(kBnThreads), 0, st, a);
     } else {
@@ -315,9 +320,11 @@ int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, 
            const float *invstd, float *gz, float *ggamma, float *gbeta, float *gbias, int C, int64_t P, int act,
            double *part, hipStream_t st, int lip = 1, int accum = 0) {
     const int S = bn_split(P);
-    const int chunk = (int)((P + S - 1) / S);
+    const int vec = (P % 4 == 0 && al16(gy) && al16(y) && al16(z) && al16(gz)) ? 1 : 0;
+    int chunk = (int)((P + S - 1) / S);
+    if (vec) chunk = (chunk + 3) & ~3;
     BnBwdArgs a{gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, part, C, (int)P, S, chunk,
-                gamma ? 1 : 0, act, lip, accum};
+                gamma ? 1 : 0, act, lip, accum, vec};
     if ((gamma || gbias) && S == 1) {
         hipLaunchKernelGGL(k_bn_bwd1, dim3(1, C), dim3(kBnThreads), 0, st, a);
     } else {
