@@ -579,6 +579,7 @@ __device__ __forceinline__ double block_sum_d(double v, double *red) {
 // Forward = k_bn_stats + k_bn_apply; backward = k_bn_bwd_stats + k_bn_bwd_apply.
 // ------------------------------------------------------------------------------------------
 constexpr int kBnThreads = 256;
+constexpr int kBn1Threads = 1024;   // one workgroup per channel (S == 1): 16 waves share the channel
 
 // c = max(max|gamma_orig|, 1.0) (lipschitz_constraint_layer.py:93-97); whole block, C <= 4 * blockDim
 __device__ float bn_lip_scale(const float *gamma, int C, float *redf) {
@@ -722,9 +723,9 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_apply(BnArgs a) {
 
 // S == 1 (a channel fits one workgroup): statistics and apply in one launch, the same
 // arithmetic as k_bn_stats + k_bn_apply (0 + the single partial)
-__global__ __launch_bounds__(kBnThreads) void k_bn_fwd1(BnArgs a) {
-    __shared__ double red[2 * kBnThreads / 64];
-    __shared__ float redf[kBnThreads / 64];
+__global__ __launch_bounds__(kBn1Threads) void k_bn_fwd1(BnArgs a) {
+    __shared__ double red[2 * kBn1Threads / 64];
+    __shared__ float redf[kBn1Threads / 64];
     __shared__ float st_s[2];
     const int c = blockIdx.y;
     double s1, s2;
@@ -878,9 +879,9 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_apply(BnBwdArgs a) {
 }
 
 // S == 1: statistics and apply in one launch (same arithmetic as the two-kernel path)
-__global__ __launch_bounds__(kBnThreads) void k_bn_bwd1(BnBwdArgs a) {
-    __shared__ double red[2 * kBnThreads / 64];
-    __shared__ float redf[kBnThreads / 64];
+__global__ __launch_bounds__(kBn1Threads) void k_bn_bwd1(BnBwdArgs a) {
+    __shared__ double red[2 * kBn1Threads / 64];
+    __shared__ float redf[kBn1Threads / 64];
     __shared__ float st_s[2];
     const int c = blockIdx.y;
     double o[3];

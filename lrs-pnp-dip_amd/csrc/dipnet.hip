@@ -76,7 +76,7 @@ Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision, bo
     const int64_t tiles = big ? t128 : (int64_t)((M + kBM64 - 1) / kBM64) * ((N + kBN64 - 1) / kBN64);
     int S = 1;
     if (tiles < 256) {
-        S = (int)((512 + tiles - 1) / tiles);
+        S = (int)((512 + tiles - 1) / tiles);   // ~2 workgroups per CU (256 and 1024 measured slower)
         const int smax = deep ? K / 512 : (K + 127) / 128;
         if (S > smax) S = smax;
         if (S > (deep ? 256 : 64)) S = deep ? 256 : 64;
@@ -307,7 +307,7 @@ int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, floa
     BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, part, C, (int)P, S, chunk, gamma ? 1 : 0, act, eps, mom, lip,
              vec};
     if (gamma && S == 1) {
-        hipLaunchKernelGGL(k_bn_fwd1, dim3(1, C), dim3(kBnThreads), 0, st, a);
+        hipLaunchKernelGGL(k_bn_fwd1, dim3(1, C), dim3(kBn1Threads), 0, st, a);
     } else {
         if (gamma) hipLaunchKernelGGL(k_bn_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
         hipLaunchKernelGGL(k_bn_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
@@ -326,7 +326,7 @@ int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, 
     BnBwdArgs a{gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, part, C, (int)P, S, chunk,
                 gamma ? 1 : 0, act, lip, accum, vec};
     if ((gamma || gbias) && S == 1) {
-        hipLaunchKernelGGL(k_bn_bwd1, dim3(1, C), dim3(kBnThreads), 0, st, a);
+        hipLaunchKernelGGL(k_bn_bwd1, dim3(1, C), dim3(kBn1Threads), 0, st, a);
     } else {
         if (gamma || gbias) hipLaunchKernelGGL(k_bn_bwd_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
         hipLaunchKernelGGL(k_bn_bwd_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
