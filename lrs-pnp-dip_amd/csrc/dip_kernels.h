@@ -1125,19 +1125,42 @@ __global__ void k_sn_apply(const SnConv *convs, const float *scale) {
 // Loss: mse(target*mask, out*mask) over C*P (main_LRS_PnP_DIP_1-LiP.py:234); gout = dL/dout.
 // mask is [P] (broadcast over channels, mask_bkg (1,1,H,W)) or null.
 // ------------------------------------------------------------------------------------------
-__global__ void k_masked_mse(const float *__restrict__ out, const float *__restrict__ target,
-                             const float *__restrict__ mask, int C, int64_t P, float *__restrict__ gout,
-                             double *loss_acc) {
+// grid (S, C): workgroup (sb, c) covers pixels [sb*chunk, +chunk) of channel c, so the mask
+// index is the pixel (no 64-bit modulo); vec: float4 loads / stores (P, chunk multiples of 4).
+__global__ __launch_bounds__(256) void k_masked_mse(const float *__restrict__ out, const float *__restrict__ target,
+                                                    const float *__restrict__ mask, int C, int64_t P, int chunk,
+                                                    int vec, float *__restrict__ gout, double *loss_acc) {
     __shared__ double red[8];
-    const int64_t N = (int64_t)C * P;
-    const float norm = (float)(2.0 / (double)N);
+    const float norm = (float)(2.0 / ((double)C * (double)P));
+    const int64_t off = (int64_t)blockIdx.y * P;
+    const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(P, i0 + chunk);
     double s = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
-        const float mk = mask ? mask[i % P] : 1.0f;
-        const float a = target[i] * mk, b = out[i] * mk;
-        const float d = a - b;
-        s += (double)d * (double)d;
-        if (gout) gout[i] = (-(norm * d)) * mk;
+    if (vec) {
+        const float4 *o4 = reinterpret_cast<const float4 *>(out + off), *t4 = reinterpret_cast<const float4 *>(target + off);
+        const float4 *m4 = reinterpret_cast<const float4 *>(mask);
+        float4 *g4 = gout ? reinterpret_cast<float4 *>(gout + off) : nullptr;
+        for (int64_t q = (i0 >> 2) + threadIdx.x; q < (i1 >> 2); q += blockDim.x) {
+            const float4 ov = o4[q], tv = t4[q];
+            const float4 mv = mask ? m4[q] : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+            const float oe[4] = {ov.x, ov.y, ov.z, ov.w}, te[4] = {tv.x, tv.y, tv.z, tv.w},
+                        me[4] = {mv.x, mv.y, mv.z, mv.w};
+            float ge[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = te[e] * me[e] - oe[e] * me[e];
+                s += (double)d * (double)d;
+                ge[e] = (-(norm * d)) * me[e];
+            }
+            if (g4) g4[q] = make_float4(ge[0], ge[1], ge[2], ge[3]);
+        }
+    } else {
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+            const float mk = mask ? mask[i] : 1.0f;
+            const float a = target[off + i] * mk, b = out[off + i] * mk;
+            const float d = a - b;
+            s += (double)d * (double)d;
+            if (gout) gout[off + i] = (-(norm * d)) * mk;
+        }
     }
     s = block_sum_d(s, red);
     if (threadIdx.x == 0) atomicAdd(loss_acc, s);

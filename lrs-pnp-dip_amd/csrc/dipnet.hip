@@ -601,8 +601,14 @@ extern "C" int lrs_adam_f32(float *p, const float *g, float *m, float *v, int64_
 extern "C" int lrs_masked_mse_f32(const float *out, const float *target, const float *mask, int C, int64_t P,
                                   float *gout, double *loss_acc, void *stream) {
     if (!out || !target || !loss_acc || C <= 0 || P <= 0) return LRS_E_INVALID;
-    hipLaunchKernelGGL(k_masked_mse, dim3(ew_blocks((int64_t)C * P, 2048)), dim3(kEw), 0, (hipStream_t)stream, out,
-                       target, mask, C, P, gout, loss_acc);
+    const int vec = (P % 4 == 0 && al16(out) && al16(target) && (!mask || al16(mask)) && (!gout || al16(gout))) ? 1 : 0;
+    int64_t S = (512 + C - 1) / C;   // ~512 workgroups over the C channels (fewer loss atomics)
+    S = std::max<int64_t>(1, std::min<int64_t>(S, (P + 1023) / 1024));
+    int64_t chunk = (P + S - 1) / S;
+    if (vec) chunk = (chunk + 3) & ~(int64_t)3;
+    if (chunk > INT32_MAX || C > 65535) return LRS_E_UNSUPPORTED;
+    hipLaunchKernelGGL(k_masked_mse, dim3((unsigned)S, (unsigned)C), dim3(256), 0, (hipStream_t)stream, out, target,
+                       mask, C, P, (int)chunk, vec, gout, loss_acc);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }

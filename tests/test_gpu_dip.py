@@ -217,16 +217,18 @@ def test_adam_matches_torch(L):
         assert rel(pd, p.detach()) < 1e-6
 
 
-def test_masked_mse(L):
+@pytest.mark.parametrize("C,H,W", [(128, 36, 36), (7, 35, 37), (198, 196, 196)])
+def test_masked_mse(L, C, H, W):
+    """Both kernel paths: float4 (H*W % 4 == 0) and scalar (35x37), one to many workgroups per channel."""
     g = torch.Generator().manual_seed(3)
-    out, tgt = torch.randn(128, 36, 36, generator=g), torch.randn(128, 36, 36, generator=g)
-    mask = (torch.rand(36, 36, generator=g) > 0.3).float()
+    out, tgt = torch.randn(C, H, W, generator=g), torch.randn(C, H, W, generator=g)
+    mask = (torch.rand(H, W, generator=g) > 0.3).float()
     o = out.clone().requires_grad_(True)
     loss = F.mse_loss(tgt * mask, o * mask)
     loss.backward()
     acc = torch.zeros(1, dtype=torch.float64, device="cuda")
-    gout = torch.empty(128, 36, 36, device="cuda")
-    assert L.lrs_masked_mse_f32(P(out.cuda()), P(tgt.cuda()), P(mask.cuda()), 128, 1296, P(gout), P(acc), S()) == 0
+    gout = torch.empty(C, H, W, device="cuda")
+    assert L.lrs_masked_mse_f32(P(out.cuda()), P(tgt.cuda()), P(mask.cuda()), C, H * W, P(gout), P(acc), S()) == 0
     torch.cuda.synchronize()
     assert abs(float(acc) / out.numel() - float(loss.detach())) < 1e-6 * float(loss.detach())
     assert rel(gout, o.grad) < 1e-6
