@@ -1183,14 +1183,34 @@ __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float
     }
     __syncthreads();
     const float step_size = sc[0], bc2s = sc[1];
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float gi = g[i];
-        const float mi = m[i] + (1.0f - b1) * (gi - m[i]);          // exp_avg.lerp_(grad, 1-b1)
-        const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;         // mul_(b2).addcmul_(g, g, 1-b2)
+    // elementwise, so the float4 body (all four buffers 16-B aligned) is bitwise the scalar one
+    auto upd = [&](float &pi, float gi, float &mi, float &vi) {
+        mi = mi + (1.0f - b1) * (gi - mi);                          // exp_avg.lerp_(grad, 1-b1)
+        vi = vi * b2 + (1.0f - b2) * gi * gi;                       // mul_(b2).addcmul_(g, g, 1-b2)
+        const float den = sqrtf(vi) / bc2s + eps;
+        pi = pi - step_size * (mi / den);
+    };
+    const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
+    const int64_t n4 = vec ? n / 4 : 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+        float4 pv = reinterpret_cast<float4 *>(p)[q], mv = reinterpret_cast<float4 *>(m)[q],
+               vv = reinterpret_cast<float4 *>(v)[q];
+        const float4 gv = reinterpret_cast<const float4 *>(g)[q];
+        upd(pv.x, gv.x, mv.x, vv.x);
+        upd(pv.y, gv.y, mv.y, vv.y);
+        upd(pv.z, gv.z, mv.z, vv.z);
+        upd(pv.w, gv.w, mv.w, vv.w);
+        reinterpret_cast<float4 *>(m)[q] = mv;
+        reinterpret_cast<float4 *>(v)[q] = vv;
+        reinterpret_cast<float4 *>(p)[q] = pv;
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float pi = p[i], mi = m[i], vi = v[i];
+        upd(pi, g[i], mi, vi);
         m[i] = mi;
         v[i] = vi;
-        const float den = sqrtf(vi) / bc2s + eps;
-        p[i] = p[i] - step_size * (mi / den);
+        p[i] = pi;
     }
 }
 

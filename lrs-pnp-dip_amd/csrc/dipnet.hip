@@ -592,7 +592,7 @@ extern "C" int lrs_adam_f32(float *p, const float *g, float *m, float *v, int64_
                             float beta1, float beta2, float eps, void *stream) {
     if (!p || !g || !m || !v || !step || n < 0) return LRS_E_INVALID;
     if (n == 0) return LRS_OK;
-    hipLaunchKernelGGL(k_adam, dim3(ew_blocks(n, 8192)), dim3(kEw), 0, (hipStream_t)stream, p, g, m, v, n, step, lr,
+    hipLaunchKernelGGL(k_adam, dim3(ew_blocks((n + 3) / 4, 8192)), dim3(kEw), 0, (hipStream_t)stream, p, g, m, v, n, step, lr,
                        beta1, beta2, eps);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
