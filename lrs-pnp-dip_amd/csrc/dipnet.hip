@@ -868,7 +868,10 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     net->W = W;
     auto fail = [&](int rc) { delete net; return rc; };
     net->implicit = g_dip_gemm_precision == LRS_DIP_SPLIT_BF16;
-    net->fork_w = (int64_t)H * W >= 65536;
+    // weight gradients on a side stream from 128^2 up: neutral alone at 196^2, but beside the
+    // concurrent sparse-coding kernel the second stream keeps the DIP its share of the chip
+    // (configs[2] 4.73 -> 5.19 outer it/s); slower at 36^2 (1.03 -> 1.19 ms per step)
+    net->fork_w = (int64_t)H * W >= 16384;
     int64_t pofs = 0, rofs = 0, ofs = 0, max_dz = 0, max_dcol = 0, part = 0, max_bnpart = 0;
     int n_sn = 0;
     for (int i = 0; i < n_nodes; ++i) {
