@@ -1218,6 +1218,13 @@ __global__ void k_counter_inc(int *c) {
     if (threadIdx.x == 0 && blockIdx.x == 0) *c += 1;
 }
 
+__global__ void k_step_begin(double *loss_acc, int *step) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        *loss_acc = 0.0;
+        *step += 1;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Early stopping (main_LRS_PnP_DIP_1-LiP.py:71-99, 244-264), on device.
 // ring: [size][N] of the last outputs; slot = (count-1) % size holds the newest.

@@ -750,8 +750,9 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
     const int n = (int)net->nodes.size();
     const auto &Lst = net->nodes[n - 1];
     const float *out = net->f(Lst.out_off);
-    hipError_t e = hipMemsetAsync(net->loss_acc(), 0, sizeof(double), st);
-    if (e != hipSuccess) return (int)e;
+    // one tiny launch zeroes the loss accumulator and advances Adam's step counter (read only by
+    // this step's k_adam)
+    hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, st, net->loss_acc(), net->step());
     rc = lrs_masked_mse_f32(out, target, mask, Lst.C, Lst.P, net->f(Lst.grad_off), net->loss_acc(), st);
     if (rc) return rc;
     // gradient buffers: the first contribution to a tensor writes, later ones accumulate
@@ -838,7 +839,6 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
         if (e == hipSuccess) e = hipStreamWaitEvent(st, net->ev_join, 0);
         if (e != hipSuccess) return (int)e;
     }
-    hipLaunchKernelGGL(k_counter_inc, dim3(1), dim3(64), 0, st, net->step());
     rc = lrs_adam_f32(net->params, net->grads, net->am, net->av, net->n_params, net->step(), lr, b1, b2, eps, st);
     if (rc) return rc;
     if (es) {
