@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group: nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--split-cube", action="store_true",
                     help="one cube over all ranks in pixel-row slabs (strong scaling; SVT Gram all-reduce)")
     ap.add_argument("--workload", default="pnp", choices=["pnp", "dip", "dip-pro"],
@@ -137,7 +139,7 @@ def main_dip(args):
     from lrspnp import dist as D
     from lrspnp.dip import DipConfig
     from lrspnp.metrics import mpsnr
-    ctx = D.init_from_env("nccl")
+    ctx = D.init_from_env(args.backend)
     pro = args.workload == "dip-pro"
     H = W = 512 if pro else 196
     B = 224 if pro else 198
@@ -196,7 +198,7 @@ def main():
     import torch
 
     from lrspnp import dist as D
-    ctx = D.init_from_env("nccl")
+    ctx = D.init_from_env(args.backend)
     from lrspnp import LrsPnP, LrsPnPConfig, ops
     from lrspnp.metrics import mpsnr
 
@@ -252,7 +254,7 @@ def main():
     ista_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     mp1 = cube_mpsnr()
     world, rank = ctx.world, ctx.rank
-    mps = D.gather_scalars([mp0, mp1], ctx)
+    mps = [[mp0, mp1]] if split else D.gather_scalars([mp0, mp1], ctx)   # split: one cube, MPSNR on rank 0
 
     n, K, nb = args.bb * args.bb, args.K, s.nb
     flops = args.nit * nb * 4 * n * K + nb * 2 * n * K
