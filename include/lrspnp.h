@@ -89,10 +89,23 @@ int lrs_ista_alpha_f32(const float *D, int64_t n, int64_t K, const uint8_t *obs_
  * Yb, obs: [nb][n_pad]; D: n x K; alpha[nb], thr[nb].  x0 = 0; Nit iterations of
  *   g = x + D^T(obs .* (y - D x)) / alpha ;  x = prox(g)
  * then phi[j*n_pad + r] = (D x_j)[r] for r < n (all rows, the inpainting step).
- * coefs (nullable) receives x [nb][K].  Supported: K = 256, n_pad % 16 == 0. */
+ * coefs (nullable) receives x [nb][K].  Any n (n_pad % 16 == 0), 1 <= K <= 512, every prox.
+ * n_pad <= 64 with K = 256 runs the dictionary-resident kernels (ws unused); everything else runs
+ * the row-split kernel, whose fragment-ordered dictionary images live in `ws`
+ * (lrs_ista_workspace bytes; LRS_E_WORKSPACE when too small).
+ * Replaces the per-block loop of main_LRS_PnP.py:270-303 / main_LRS_PnP_DIP_1-LiP.py:367-392
+ * around ista() (main_LRS_PnP.py:131-149, …1-LiP.py:185-198) and delete_element (:201-204). */
+size_t lrs_ista_workspace(int64_t n, int64_t K, int prox);
 int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,
                  int64_t K, int64_t nb, const float *alpha, const double *thr, int Nit, int prox,
-                 float *coefs, float *phi, void *stream);
+                 float *coefs, float *phi, void *ws, size_t ws_bytes, void *stream);
+/* Column tiles (16 blocks each) per wave of the row-split kernel at 129 <= K <= 256: 1 (default,
+ * more waves) or 2 (each dictionary fragment serves 32 blocks).  Process-wide. */
+int lrs_ista_set_rs_cols(int cols);
+/* NLmeansfilter(g, 3, 3, h) (LRS-PnP(Matlab Code)/NLmeansfilter.m:18-78, the prox of
+ * pnp_ista.m:30) of nvec columns of length K, fp64, 'symmetric' padding. */
+int lrs_nlm_matlab_col_f32(const float *g, int64_t ldg, float *out, int64_t ldo, int64_t K,
+                           int64_t nvec, double h, const double *h_per_vec, void *stream);
 /* Arithmetic of the two products of the resident (n_pad <= 64) kernel, process-wide:
  * LRS_ISTA_SPLIT_BF16 (default): bf16 matrix cores on operands split exactly into three bf16
  * terms (six partial products, fp32 accumulation: fp32-GEMM accuracy, not bitwise the f32 MFMA);

@@ -215,94 +215,6 @@ __device__ __forceinline__ void nlm_prox_registers(const floatx4 (&G)[K / 16], f
     }
 }
 
-// MATLAB-variant prox (LRS-PnP(Matlab Code)/pnp_ista.m:30: NLmeansfilter(gradient, 3, 3, 0.1 T),
-// NLmeansfilter.m:18-78), fp64, along the atom axis: 'symmetric' padding, a 7-row similarity
-// window weighted by the row sums krow of make_kernel(3), exp(-d/h^2) weights over the 6 nearest
-// atoms, the centre weighted by the largest of them.  A chunk of 4 atoms needs atoms a-6 .. a+9:
-// chunks c-2 .. c+2, i.e. lanes l-32 .. l+32 of tiles q-1 .. q+1.  Same evaluation order as
-// oracle/nlm_oracle.c:oracle_nlm_matlab_col.
-__device__ __forceinline__ void nlm_matlab_krow(double (&krow)[7]) {
-#pragma unroll
-    for (int u = -3; u <= 3; ++u) {
-        const int a = u < 0 ? -u : u;
-        double s = 0.0;
-        for (int d = (a < 1 ? 1 : a); d <= 3; ++d) s = s + 1.0 / (double)(2 * d + 1);
-        krow[u + 3] = s / 3.0;
-    }
-}
-
-template <int K>
-__device__ __forceinline__ void nlm_matlab_prox_registers(const floatx4 (&G)[K / 16], float (&X)[K / 16][4],
-                                                          double h, int lane) {
-    constexpr int NQ = K / 16, NC = K / 4;
-    const int g = lane >> 4;
-    const int p1 = (lane + 48) & 63, p2 = (lane + 32) & 63, n1 = (lane + 16) & 63;
-    double krow[7];
-    nlm_matlab_krow(krow);
-    const double h2 = h * h;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int qp = q > 0 ? q - 1 : 0, qn = q + 1 < NQ ? q + 1 : NQ - 1;
-        float w[16];
-        // chunk c-2 (last two atoms), c-1, own, c+1, c+2 (first two atoms)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float cur = __shfl(G[q][2 + e], p2, 64), prv = __shfl(G[qp][2 + e], p2, 64);
-            w[e] = g >= 2 ? cur : prv;
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float cur = __shfl(G[q][e], p1, 64), prv = __shfl(G[qp][e], p1, 64);
-            w[2 + e] = g >= 1 ? cur : prv;
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[6 + e] = G[q][e];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float cur = __shfl(G[q][e], n1, 64), nxt = __shfl(G[qn][e], n1, 64);
-            w[10 + e] = g <= 2 ? cur : nxt;
-        }
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float cur = __shfl(G[q][e], p2, 64), nxt = __shfl(G[qn][e], p2, 64);
-            w[14 + e] = g <= 1 ? cur : nxt;
-        }
-        // symmetric padding: g-hat[j] = g[-j-1] (j < 0), g[2K-1-j] (j >= K)
-        const int c = 4 * q + g;
-        if (c == 0) { w[2] = w[9]; w[3] = w[8]; w[4] = w[7]; w[5] = w[6]; }
-        if (c == 1) { w[0] = w[3]; w[1] = w[2]; }
-        if (c == NC - 1) { w[10] = w[9]; w[11] = w[8]; w[12] = w[7]; w[13] = w[6]; }
-        if (c == NC - 2) { w[14] = w[13]; w[15] = w[12]; }
-        double v[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) v[e] = (double)w[e];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int i = 4 * c + e, p = 6 + e;
-            double sw = 0.0, av = 0.0, wmax = 0.0;
-#pragma unroll
-            for (int t = -3; t <= 3; ++t) {
-                if (t == 0) continue;
-                const int r = i + t;
-                if (r < 0 || r >= K) continue;
-                double d = 0.0;
-#pragma unroll
-                for (int u = -3; u <= 3; ++u) {
-                    const double df = v[p + u] - v[p + t + u];
-                    d = d + krow[u + 3] * (df * df);
-                }
-                const double wt = exp(-d / h2);
-                if (wt > wmax) wmax = wt;
-                sw = sw + wt;
-                av = av + wt * v[p + t];
-            }
-            av = av + wmax * v[p];
-            sw = sw + wmax;
-            X[q][e] = sw > 0.0 ? (float)(av / sw) : w[p];
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // Resident kernel (n_pad <= 64, i.e. bb <= 8): dictionary in LDS for the whole launch, y and the
 // row mask in VGPRs, and a software pipeline over the 16 atom tiles q of each inner iteration:
@@ -619,79 +531,6 @@ struct Reuse6 {
     int v[6];   // W1[6], W2[5], W2[6], W3[4], W3[5], W3[6] of a chunk
 };
 
-template <int DIV>
-__device__ __forceinline__ float nlm_div_v(double num, double den) {
-    double r = __builtin_amdgcn_rcp(den);
-    if (DIV == 0) return (float)(num * r);
-    const double e = __fma_rn(-den, r, 1.0);
-    r = __fma_rn(r, e, r);
-    return (float)(num * r);
-}
-
-__device__ __forceinline__ float nlm_div_fast(double num, double den) {
-    double r = __builtin_amdgcn_rcp(den);
-    const double e = __fma_rn(-den, r, 1.0);
-    r = __fma_rn(r, e, r);
-    const double q = num * r;
-    const double rem = __fma_rn(-den, q, num);
-    return (float)__fma_rn(rem, r, q);
-}
-
-// W_t[i] = weight(s_t(i) + s_t(i+1)), s_t(k) = (w[k] - w[k+t])^2, for i >= i0 (FULL: all 18)
-template <bool FULL>
-__device__ __forceinline__ void nlm_weights(const double (&w)[11], double kneg, int (&W1)[7], int (&W2)[7],
-                                            int (&W3)[7]) {
-    {
-        constexpr int i0 = FULL ? 2 : 3;
-        double sp = (w[i0] - w[i0 + 1]) * (w[i0] - w[i0 + 1]);
-#pragma unroll
-        for (int i = i0; i < 7; ++i) {
-            const double d = w[i + 1] - w[i + 2], sn = d * d;
-            W1[i] = nlm_weight_hi(sp + sn, kneg);
-            sp = sn;
-        }
-    }
-    {
-        constexpr int i0 = FULL ? 1 : 3;
-        double sp = (w[i0] - w[i0 + 2]) * (w[i0] - w[i0 + 2]);
-#pragma unroll
-        for (int i = i0; i < 7; ++i) {
-            const double d = w[i + 1] - w[i + 3], sn = d * d;
-            W2[i] = nlm_weight_hi(sp + sn, kneg);
-            sp = sn;
-        }
-    }
-    {
-        constexpr int i0 = FULL ? 0 : 3;
-        double sp = (w[i0] - w[i0 + 3]) * (w[i0] - w[i0 + 3]);
-#pragma unroll
-        for (int i = i0; i < 7; ++i) {
-            const double d = w[i + 1] - w[i + 4], sn = d * d;
-            W3[i] = nlm_weight_hi(sp + sn, kneg);
-            sp = sn;
-        }
-    }
-}
-
-template <int DIV = 2>
-__device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W1)[7], const int (&W2)[7],
-                                            const int (&W3)[7], double c0, double seven, float (&out)[4]) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int C = 3 + e;
-        const double ws[6] = {hi_to_double(W3[C - 3]), hi_to_double(W2[C - 2]), hi_to_double(W1[C - 1]),
-                              hi_to_double(W1[C]), hi_to_double(W2[C]), hi_to_double(W3[C])};
-        const double vs[6] = {w[C - 3], w[C - 2], w[C - 1], w[C + 1], w[C + 2], w[C + 3]};
-        double swv = 0.0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) swv = __fma_rn(ws[k], vs[k], swv);   // canonical order
-        const double sw = ((ws[0] + ws[5]) + (ws[1] + ws[4])) + (ws[2] + ws[3]);   // exact
-        const double num = __fma_rn(seven, swv, c0 * w[C]);
-        const double den = __fma_rn(seven, sw, c0);
-        out[e] = DIV == 2 ? nlm_div_fast(num, den) : nlm_div_v<DIV>(num, den);
-    }
-}
-
 // tile q of the NLM with weight reuse (FULL for the first tile, whose g == 0 chunk has a
 // reflected window).  `carry`: this lane's trailing weights of tile q-1 on entry, of tile q on
 // exit; only the g == 3 lanes' copy is read (by the g == 0 lanes of the next tile).
@@ -1007,170 +846,6 @@ __device__ __forceinline__ void nlm_chunk_ln(const float (&prv)[3], const floatx
     carry[1] = W2[5]; carry[2] = W2[6];
     carry[3] = W3[4]; carry[4] = W3[5]; carry[5] = W3[6];
     nlm_outputs(w, W1, W2, W3, c0, seven, out);
-}
-
-template <int K, bool SOFT, int LA = 2, int EXP = 0>
-__global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln(IstaParams p) {
-    static_assert(K == 256, "the lane layout assumes 4 groups of 64 atoms");
-    constexpr int NQ = K / 16;
-    __shared__ __attribute__((aligned(16))) IstaSmemB3<K> S;
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int jl = lane & 15, g = lane >> 4;
-    const int64_t j = ((int64_t)blockIdx.x * kB3Waves + wave) * 16 + jl;
-    const bool valid = j < p.nb;
-    const int NT = p.n_pad / 16;
-    const int src_prev = (lane + 48) & 63, src_next = (lane + 16) & 63;
-
-    const float alpha = valid ? p.alpha[j] : 1.0f;
-    const double thr = valid ? p.thr[j] : 1.0;
-    const double kneg = nlm_kneg(thr);
-    const double c0 = nlm_c0();
-    const float Tsoft = (float)thr;
-
-    float y[4][4];
-    uint32_t mres = 0;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        float4 yv = {0.f, 0.f, 0.f, 0.f};
-        uint32_t mv = 0;
-        if (valid && t < NT) {
-            yv = *reinterpret_cast<const float4 *>(&p.Yb[j * p.n_pad + 16 * t + 4 * g]);
-            mv = *reinterpret_cast<const uint32_t *>(&p.obs[j * p.n_pad + 16 * t + 4 * g]);
-        }
-        y[t][0] = yv.x; y[t][1] = yv.y; y[t][2] = yv.z; y[t][3] = yv.w;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) mres |= (((mv >> (8 * i)) & 0xffu) ? 1u : 0u) << (4 * t + i);
-    }
-    stage_dictionary_ln<K, kB3Threads>(S, p.D, p.n);
-    __syncthreads();
-
-    float X[NQ][4];   // X[q][i] = coefficient of atom 64g + 4q + i
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) X[q][0] = X[q][1] = X[q][2] = X[q][3] = 0.f;
-    floatx4 R[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    const float ainv = 1.0f / alpha;
-    auto gradient = [&](floatx4 &Gq, const float (&xq)[4]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Gq[i] = xq[i] + div_by(Gq[i], alpha, ainv);
-    };
-    auto soft = [&](const floatx4 &Gq, float (&o)[4]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float t = fabsf(Gq[i]) - Tsoft;
-            t = t > 0.f ? t : 0.f;
-            o[i] = Gq[i] > 0.f ? t : (Gq[i] < 0.f ? -t : 0.f);
-        }
-    };
-
-    for (int it = 0; it < p.Nit; ++it) {
-        float r[4][4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) r[t][i] = ((mres >> (4 * t + i)) & 1u) ? (y[t][i] - R[t][i]) : 0.0f;
-            R[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-        bf16x8 rf[2][3];
-        split_frag(r[0], r[1], rf[0]);
-        split_frag(r[2], r[3], rf[1]);
-        // prologue: tile 15 (whose last atoms are the next group's left neighbours) and tiles 0..3;
-        // step p then runs the products of tiles 2p+4, 2p+5 (<= 14) and the D x of pair p-1 beside
-        // the NLM of tiles 2p, 2p+1
-        floatx4 G[NQ];
-        constexpr int QL = NQ;   // tile 15 is recomputed in the pipeline (its early copy only feeds the edge)
-#pragma unroll
-        for (int q = 0; q < 2 * LA; ++q) G[q] = ln_gemm2<K>(S, q, rf, lane);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 2 * LA; ++q) gradient(G[q], X[q]);
-        float edge_prev[3], edge_next[4];
-        if (!SOFT) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) edge_next[e] = __shfl(G[0][e], src_next, 64);
-        }
-        int carry[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int pp = 0; pp < NQ / 2; ++pp) {
-            const int qa = 2 * pp, qb = qa + 1;
-            if (qa + 2 * LA < QL) G[qa + 2 * LA] = ln_gemm2<K>(S, qa + 2 * LA, rf, lane);
-            if (qb + 2 * LA < QL) G[qb + 2 * LA] = ln_gemm2<K>(S, qb + 2 * LA, rf, lane);
-            if (pp == 0) {  // tile 15's last atoms are the next group's left neighbours
-                floatx4 G15 = ln_gemm2<K>(S, NQ - 1, rf, lane);
-                gradient(G15, X[NQ - 1]);
-                if (!SOFT) {
-#pragma unroll
-                    for (int e = 0; e < 3; ++e) {
-                        const float v = __shfl(G15[e + 1], src_prev, 64);
-                        edge_prev[e] = (g == 0) ? G[0][3 - e] : v;      // reflect: atoms -3,-2,-1 -> 3,2,1
-                    }
-                }
-            }
-            if (pp > 0) {   // D x of the previous pair beside this pair's NLM
-                bf16x8 xf[3];
-                split_frag(X[qa - 2], X[qb - 2], xf);
-                ln_gemm1<K>(S, pp - 1, xf, R, lane);
-            }
-            float oa[4], ob[4];
-            if (SOFT) {
-                soft(G[qa], oa);
-                soft(G[qb], ob);
-            } else {
-                float prv[3], nxt[4];
-                if (qa == 0) {
-#pragma unroll
-                    for (int e = 0; e < 3; ++e) prv[e] = edge_prev[e];
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 3; ++e) prv[e] = G[qa - 1][e + 1];
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) nxt[e] = G[qb][e];
-                if (qa == 0 || (EXP & 2)) nlm_chunk_ln<true>(prv, G[qa], nxt, kneg, c0, p.seven, carry, oa);
-                else nlm_chunk_ln<false>(prv, G[qa], nxt, kneg, c0, p.seven, carry, oa);
-                if (EXP & 1) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int e = 0; e < 3; ++e) prv[e] = G[qa][e + 1];
-                if (qb == NQ - 1) {    // reflect: atoms 256..259 -> 254, 253, 252, 251
-                    const float rfl[4] = {G[qb][2], G[qb][1], G[qb][0], G[qa][3]};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) nxt[e] = (g == 3) ? rfl[e] : edge_next[e];
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) nxt[e] = G[qb + 1][e];
-                }
-                if (EXP & 2) nlm_chunk_ln<true>(prv, G[qb], nxt, kneg, c0, p.seven, carry, ob);
-                else nlm_chunk_ln<false>(prv, G[qb], nxt, kneg, c0, p.seven, carry, ob);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { X[qa][i] = oa[i]; X[qb][i] = ob[i]; }
-            if (qa + 2 * LA < QL) gradient(G[qa + 2 * LA], X[qa + 2 * LA]);
-            if (qb + 2 * LA < QL) gradient(G[qb + 2 * LA], X[qb + 2 * LA]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        {
-            bf16x8 xf[3];
-            split_frag(X[NQ - 2], X[NQ - 1], xf);
-            ln_gemm1<K>(S, NQ / 2 - 1, xf, R, lane);
-        }
-    }
-
-    if (valid) {
-        if (p.coefs) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q)
-                *reinterpret_cast<float4 *>(&p.coefs[j * K + 64 * g + 4 * q]) =
-                    make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            if (t < NT)
-                *reinterpret_cast<float4 *>(&p.phi[j * p.n_pad + 16 * t + 4 * g]) =
-                    make_float4(R[t][0], R[t][1], R[t][2], R[t][3]);
-    }
 }
 
 // ---- explicitly scheduled lane-layout kernel -------------------------------------------------------
@@ -1493,133 +1168,6 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln2(IstaParams p) {
     }
 }
 
-template <int K, bool RESIDENT>
-__global__ __launch_bounds__(kIstaThreads, 2) void k_ista(IstaParams p) {
-    constexpr int NQ = K / 16;
-    __shared__ __attribute__((aligned(16))) IstaSmem<K> S;
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int jl = lane & 15, g = lane >> 4;
-    const int64_t j = ((int64_t)blockIdx.x * kIstaWaves + wave) * 16 + jl;
-    const bool valid = j < p.nb;
-    const int NT = p.n_pad / 16;
-    const int nstage = (p.n_pad + kStageRows - 1) / kStageRows;
-
-    const float alpha = valid ? p.alpha[j] : 1.0f;
-    const double thr = valid ? p.thr[j] : 1.0;
-
-    float X[NQ][4];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) X[q][0] = X[q][1] = X[q][2] = X[q][3] = 0.f;
-
-    // Resident mode (n_pad <= 64): y and the row mask live in registers for all iterations.
-    float yres[4][4];
-    uint32_t mres = 0;
-    if (RESIDENT) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            float4 yv = {0.f, 0.f, 0.f, 0.f};
-            uint32_t mv = 0;
-            if (valid && t < NT) {
-                yv = *reinterpret_cast<const float4 *>(&p.Yb[j * p.n_pad + 16 * t + 4 * g]);
-                mv = *reinterpret_cast<const uint32_t *>(&p.obs[j * p.n_pad + 16 * t + 4 * g]);
-            }
-            yres[t][0] = yv.x; yres[t][1] = yv.y; yres[t][2] = yv.z; yres[t][3] = yv.w;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) mres |= (((mv >> (8 * i)) & 0xffu) ? 1u : 0u) << (4 * t + i);
-        }
-        stage_dictionary<K>(S, p.D, p.n, 0);
-        __syncthreads();
-    }
-
-    for (int it = 0; it < p.Nit; ++it) {
-        floatx4 G[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) G[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < nstage; ++s) {
-            if (!RESIDENT) {
-                __syncthreads();
-                stage_dictionary<K>(S, p.D, p.n, s * kStageRows);
-                __syncthreads();
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int T = s * 4 + t;
-                if (T >= NT) break;
-                const floatx4 acc = dict_times_x<K>(S, t, X, jl, g);
-                float y[4];
-                uint32_t m4;
-                if (RESIDENT) {
-                    y[0] = yres[t][0]; y[1] = yres[t][1]; y[2] = yres[t][2]; y[3] = yres[t][3];
-                    m4 = (mres >> (4 * t)) & 0xfu;
-                } else {
-                    float4 yv = {0.f, 0.f, 0.f, 0.f};
-                    uint32_t mv = 0;
-                    if (valid) {
-                        yv = *reinterpret_cast<const float4 *>(&p.Yb[j * p.n_pad + 16 * T + 4 * g]);
-                        mv = *reinterpret_cast<const uint32_t *>(&p.obs[j * p.n_pad + 16 * T + 4 * g]);
-                    }
-                    y[0] = yv.x; y[1] = yv.y; y[2] = yv.z; y[3] = yv.w;
-                    m4 = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) m4 |= (((mv >> (8 * i)) & 0xffu) ? 1u : 0u) << i;
-                }
-                float r[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) r[i] = ((m4 >> i) & 1u) ? (y[i] - acc[i]) : 0.0f;
-                dict_t_times_r<K>(S, t, r, G, jl, g);
-            }
-        }
-        // gradient = x + (D^T r) / alpha   (…1-LiP.py:190: torch.mm(...) / alpha, then x +)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) G[q][i] = X[q][i] + div_by(G[q][i], alpha, 1.0f / alpha);
-        }
-        if (p.prox == LRS_PROX_SOFT) {
-            const float T = (float)thr;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float gv = G[q][i];
-                    float t = fabsf(gv) - T;
-                    t = t > 0.f ? t : 0.f;
-                    X[q][i] = gv > 0.f ? t : (gv < 0.f ? -t : 0.f);
-                }
-            }
-        } else if (p.prox == LRS_PROX_NLM_MATLAB) {
-            nlm_matlab_prox_registers<K>(G, X, thr, lane);
-        } else {
-            nlm_prox_registers<K>(G, X, thr, lane);
-        }
-    }
-
-    if (valid && p.coefs) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-            *reinterpret_cast<float4 *>(&p.coefs[j * K + 16 * q + 4 * g]) =
-                make_float4(X[q][0], X[q][1], X[q][2], X[q][3]);
-    }
-    // Phi_z = Full_Dictionary @ Coefs (all rows, missing ones included: the inpainting step)
-    for (int s = 0; s < nstage; ++s) {
-        if (!RESIDENT) {
-            __syncthreads();
-            stage_dictionary<K>(S, p.D, p.n, s * kStageRows);
-            __syncthreads();
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int T = s * 4 + t;
-            if (T >= NT) break;
-            const floatx4 acc = dict_times_x<K>(S, t, X, jl, g);
-            if (valid)
-                *reinterpret_cast<float4 *>(&p.phi[j * p.n_pad + 16 * T + 4 * g]) =
-                    make_float4(acc[0], acc[1], acc[2], acc[3]);
-        }
-    }
-}
-
 // Standalone NLM over nvec columns of length K (any K >= 1): one workgroup per column, the
 // column reflect-padded in LDS, one thread per output.  Used by lrs_nlm_col_f32 (the
 // denoise_nl_means drop-in) — the fused ISTA kernel above does not call it.
@@ -1669,33 +1217,62 @@ extern "C" int lrs_ista_set_precision(int precision) {
 
 extern "C" int lrs_ista_get_precision(void) { return g_ista_precision; }
 
+// row-split kernel (csrc/ista_rs.hip): any n, K <= 512, every prox
+namespace lrs {
+size_t ista_rs_workspace(int64_t n, int64_t K);
+int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
+                   const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi, void *ws,
+                   size_t ws_bytes, int cols_per_wave, hipStream_t st);
+int nlm_matlab_col_launch(const float *g, int64_t ldg, float *out, int64_t ldo, int64_t K, int64_t nvec, double h,
+                          const double *h_per_vec, hipStream_t st);
+}  // namespace lrs
+
+static int g_ista_rs_cols = 1;   // column tiles (16 blocks) per wave of the row-split kernel
+
+extern "C" int lrs_ista_set_rs_cols(int cols) {
+    if (cols != 1 && cols != 2) return LRS_E_INVALID;
+    g_ista_rs_cols = cols;
+    return LRS_OK;
+}
+
+// The resident kernels (dictionary in LDS) serve n_pad <= 64 with K = 256 and the skimage / soft
+// prox; everything else runs the row-split kernel, which needs the fragment-ordered dictionary.
+static bool ista_resident(int64_t n_pad, int64_t K, int prox) {
+    return n_pad <= kStageRows && K == 256 && prox != LRS_PROX_NLM_MATLAB;
+}
+
+extern "C" size_t lrs_ista_workspace(int64_t n, int64_t K, int prox) {
+    if (n <= 0 || K <= 0) return 0;
+    if (ista_resident(round_up(n, 16), K, prox)) return 0;
+    return ista_rs_workspace(n, K);
+}
+
 extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n,
                             int64_t n_pad, int64_t K, int64_t nb, const float *alpha, const double *thr,
-                            int Nit, int prox, float *coefs, float *phi, void *stream) {
-    if (!Yb || !obs || !D || !alpha || !thr || !phi || n <= 0 || nb < 0 || Nit < 0) return LRS_E_INVALID;
+                            int Nit, int prox, float *coefs, float *phi, void *ws, size_t ws_bytes, void *stream) {
+    if (!Yb || !obs || !D || !alpha || !thr || !phi || n <= 0 || nb < 0 || Nit < 0 || K <= 0) return LRS_E_INVALID;
     if (n_pad % 16 != 0 || n_pad < n) return LRS_E_INVALID;
     if (prox != LRS_PROX_NLM && prox != LRS_PROX_SOFT && prox != LRS_PROX_NLM_MATLAB) return LRS_E_INVALID;
-    if (K != 256) return LRS_E_UNSUPPORTED;
-    if (nb == 0) return LRS_OK;
+    if (K > 512) return LRS_E_UNSUPPORTED;
     if (n_pad > (int64_t)1 << 20 || nb > ((int64_t)1 << 40)) return LRS_E_INVALID;
+    if (nb == 0) return LRS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (!ista_resident(n_pad, K, prox))
+        return ista_rs_launch(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes,
+                              g_ista_rs_cols, st);
     IstaParams p{Yb, obs, D, alpha, thr, coefs, phi, (int)n, (int)n_pad, Nit, prox, nb, 7.0};
     const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
     dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));
-    hipStream_t st = (hipStream_t)stream;
     const bool split = g_ista_precision == LRS_ISTA_SPLIT_BF16;
     const dim3 grid_b3((unsigned)((nb + kB3Waves * 16 - 1) / (kB3Waves * 16)));
-    if (prox == LRS_PROX_NLM_MATLAB)   // the MATLAB-variant prox lives in the streaming kernel only
-        hipLaunchKernelGGL((k_ista<256, false>), grid, dim3(kIstaThreads), 0, st, p);
-    else if (n_pad <= kStageRows && split && prox == LRS_PROX_SOFT)
+    if (split && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_b3<256, true>), grid_b3, dim3(kB3Threads), 0, st, p);
-    else if (n_pad <= kStageRows && split)
+    else if (split)
         hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, 1>), grid_b3, dim3(kB3Threads), 0, st, p);
-    else if (n_pad <= kStageRows && prox == LRS_PROX_SOFT)
+    else if (prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_res<256, true>), grid, dim3(kIstaThreads), 0, st, p);
-    else if (n_pad <= kStageRows)
-        hipLaunchKernelGGL((k_ista_res<256, false>), grid, dim3(kIstaThreads), 0, st, p);
     else
-        hipLaunchKernelGGL((k_ista<256, false>), grid, dim3(kIstaThreads), 0, st, p);
+        hipLaunchKernelGGL((k_ista_res<256, false>), grid, dim3(kIstaThreads), 0, st, p);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -1713,78 +1290,10 @@ extern "C" int lrs_nlm_col_f32(const float *g, int64_t ldg, float *out, int64_t 
     return LRS_OK;
 }
 
-// Diagnostic entry (not in include/lrspnp.h): variants of the split-bf16 kernel (timing only:
-// 1 no shuffles, 2 no NLM, 3 no MFMA products, 4 two waves per SIMD, 5 sequential tile pair NLM).
-extern "C" int lrs_diag_ista_b3_variant(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,
-                                        int64_t nb, const float *alpha, const double *thr, int Nit, int variant,
-                                        float *phi, void *stream) {
-    if (n_pad > kStageRows || !phi) return LRS_E_INVALID;
-    IstaParams p{Yb, obs, D, alpha, thr, nullptr, phi, (int)n, (int)n_pad, Nit, LRS_PROX_NLM, nb, 7.0};
-    hipStream_t st = (hipStream_t)stream;
-    const dim3 g4((unsigned)((nb + 63) / 64)), g8((unsigned)((nb + 127) / 128));
-    switch (variant) {
-    case 0: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 0>), g4, dim3(256), 0, st, p); break;
-    case 1: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 1>), g4, dim3(256), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 2>), g4, dim3(256), 0, st, p); break;
-    case 3: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 3>), g4, dim3(256), 0, st, p); break;
-    case 4: hipLaunchKernelGGL((k_ista_b3<256, false, 8, false, 0>), g8, dim3(512), 0, st, p); break;
-    case 5: hipLaunchKernelGGL((k_ista_b3<256, false, 4, true, 0>), g4, dim3(256), 0, st, p); break;
-    case 6: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 0, 1>), g4, dim3(256), 0, st, p); break;
-    case 7: hipLaunchKernelGGL((k_ista_b3<256, false, 4, false, 0, 2>), g4, dim3(256), 0, st, p); break;
-    case 8: hipLaunchKernelGGL((k_ista_ln<256, false>), g4, dim3(256), 0, st, p); break;
-    case 9: hipLaunchKernelGGL((k_ista_ln<256, false, 1>), g4, dim3(256), 0, st, p); break;
-    case 10: hipLaunchKernelGGL((k_ista_ln2<256, false>), g4, dim3(256), 0, st, p); break;
-    case 11: hipLaunchKernelGGL((k_ista_ln2<256, true>), g4, dim3(256), 0, st, p); break;
-    case 12: hipLaunchKernelGGL((k_ista_ln2<256, false, 1>), g4, dim3(256), 0, st, p); break;
-    case 13: hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true>), g4, dim3(256), 0, st, p); break;
-    case 14: hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, 1>), g4, dim3(256), 0, st, p); break;
-    case 15: hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, 0>), g4, dim3(256), 0, st, p); break;
-    default: return LRS_E_INVALID;
-    }
-    LRS_CHECK_LAUNCH();
-    return LRS_OK;
-}
-
-// Diagnostic entry (not in include/lrspnp.h): time ablated variants of the resident kernel.
-extern "C" int lrs_diag_ista_ablate_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,
-                                        int64_t nb, const float *alpha, const double *thr, int Nit, int ablate,
-                                        float *phi, void *stream) {
-    if (n_pad > kStageRows || !phi) return LRS_E_INVALID;
-    IstaParams p{Yb, obs, D, alpha, thr, nullptr, phi, (int)n, (int)n_pad, Nit, LRS_PROX_NLM, nb, 7.0};
-    const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
-    dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));
-    hipStream_t st = (hipStream_t)stream;
-    if (ablate == 1) hipLaunchKernelGGL((k_ista_res<256, false, 1>), grid, dim3(kIstaThreads), 0, st, p);
-    else if (ablate == 2) hipLaunchKernelGGL((k_ista_res<256, false, 2>), grid, dim3(kIstaThreads), 0, st, p);
-    else hipLaunchKernelGGL((k_ista_res<256, false, 0>), grid, dim3(kIstaThreads), 0, st, p);
-    LRS_CHECK_LAUNCH();
-    return LRS_OK;
-}
-
-// Diagnostics: the in-register MATLAB-variant prox alone on [nb][256] vectors (16 per wave).
-__global__ __launch_bounds__(64) void k_diag_nlm_matlab(const float *__restrict__ g, const double *__restrict__ h,
-                                                       int64_t nb, float *__restrict__ out) {
-    constexpr int K = 256, NQ = K / 16;
-    const int lane = threadIdx.x, jl = lane & 15, gq = lane >> 4;
-    const int64_t j = (int64_t)blockIdx.x * 16 + jl;
-    const bool valid = j < nb;
-    floatx4 G[NQ];
-    float X[NQ][4];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) G[q][i] = valid ? g[j * K + 16 * q + 4 * gq + i] : 0.f;
-    nlm_matlab_prox_registers<K>(G, X, valid ? h[j] : 1.0, lane);
-    if (valid)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) out[j * K + 16 * q + 4 * gq + i] = X[q][i];
-}
-
-extern "C" int lrs_diag_nlm_matlab(const float *g, const double *h, int64_t nb, float *out, void *stream) {
-    hipLaunchKernelGGL(k_diag_nlm_matlab, dim3((unsigned)((nb + 15) / 16)), dim3(64), 0, (hipStream_t)stream, g, h,
-                       nb, out);
-    LRS_CHECK_LAUNCH();
-    return LRS_OK;
+extern "C" int lrs_nlm_matlab_col_f32(const float *g, int64_t ldg, float *out, int64_t ldo, int64_t K,
+                                      int64_t nvec, double h, const double *h_per_vec, void *stream) {
+    if (!g || !out || K <= 0 || nvec < 0 || ldg < K || ldo < K) return LRS_E_INVALID;
+    if (K > 16384) return LRS_E_UNSUPPORTED;
+    if (nvec == 0) return LRS_OK;
+    return nlm_matlab_col_launch(g, ldg, out, ldo, K, nvec, h, h_per_vec, (hipStream_t)stream);
 }

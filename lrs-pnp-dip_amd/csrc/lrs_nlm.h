@@ -55,4 +55,78 @@ __device__ __forceinline__ float nlm_point(const double (&w)[11], double kneg, d
     return (float)(num / den);
 }
 
+// ---- 4-output chunk with the 18 pair weights computed once (shared by the ISTA kernels) ----
+template <int DIV>
+__device__ __forceinline__ float nlm_div_v(double num, double den) {
+    double r = __builtin_amdgcn_rcp(den);
+    if (DIV == 0) return (float)(num * r);
+    const double e = __fma_rn(-den, r, 1.0);
+    r = __fma_rn(r, e, r);
+    return (float)(num * r);
+}
+
+__device__ __forceinline__ float nlm_div_fast(double num, double den) {
+    double r = __builtin_amdgcn_rcp(den);
+    const double e = __fma_rn(-den, r, 1.0);
+    r = __fma_rn(r, e, r);
+    const double q = num * r;
+    const double rem = __fma_rn(-den, q, num);
+    return (float)__fma_rn(rem, r, q);
+}
+
+// W_t[i] = weight(s_t(i) + s_t(i+1)), s_t(k) = (w[k] - w[k+t])^2, for i >= i0 (FULL: all 18)
+template <bool FULL>
+__device__ __forceinline__ void nlm_weights(const double (&w)[11], double kneg, int (&W1)[7], int (&W2)[7],
+                                            int (&W3)[7]) {
+    {
+        constexpr int i0 = FULL ? 2 : 3;
+        double sp = (w[i0] - w[i0 + 1]) * (w[i0] - w[i0 + 1]);
+#pragma unroll
+        for (int i = i0; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 2], sn = d * d;
+            W1[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
+    {
+        constexpr int i0 = FULL ? 1 : 3;
+        double sp = (w[i0] - w[i0 + 2]) * (w[i0] - w[i0 + 2]);
+#pragma unroll
+        for (int i = i0; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 3], sn = d * d;
+            W2[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
+    {
+        constexpr int i0 = FULL ? 0 : 3;
+        double sp = (w[i0] - w[i0 + 3]) * (w[i0] - w[i0 + 3]);
+#pragma unroll
+        for (int i = i0; i < 7; ++i) {
+            const double d = w[i + 1] - w[i + 4], sn = d * d;
+            W3[i] = nlm_weight_hi(sp + sn, kneg);
+            sp = sn;
+        }
+    }
+}
+
+template <int DIV = 2>
+__device__ __forceinline__ void nlm_outputs(const double (&w)[11], const int (&W1)[7], const int (&W2)[7],
+                                            const int (&W3)[7], double c0, double seven, float (&out)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int C = 3 + e;
+        const double ws[6] = {hi_to_double(W3[C - 3]), hi_to_double(W2[C - 2]), hi_to_double(W1[C - 1]),
+                              hi_to_double(W1[C]), hi_to_double(W2[C]), hi_to_double(W3[C])};
+        const double vs[6] = {w[C - 3], w[C - 2], w[C - 1], w[C + 1], w[C + 2], w[C + 3]};
+        double swv = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) swv = __fma_rn(ws[k], vs[k], swv);   // canonical order
+        const double sw = ((ws[0] + ws[5]) + (ws[1] + ws[4])) + (ws[2] + ws[3]);   // exact
+        const double num = __fma_rn(seven, swv, c0 * w[C]);
+        const double den = __fma_rn(seven, sw, c0);
+        out[e] = DIV == 2 ? nlm_div_fast(num, den) : nlm_div_v<DIV>(num, den);
+    }
+}
+
 }  // namespace lrs

@@ -51,7 +51,10 @@ def _declare(L):
         "lrs_im2col_f32": (i32, [vp, vp, f32, i64, i64, i64, vp, vp, i64, i64, vp, vp, vp]),
         "lrs_ista_alpha_workspace": (sz, [i64, i64, i64]),
         "lrs_ista_alpha_f32": (i32, [vp, i64, i64, vp, i64, i64, i32, f32, vp, vp, vp, sz, vp]),
-        "lrs_ista_f32": (i32, [vp, vp, vp, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp, vp]),
+        "lrs_ista_workspace": (sz, [i64, i64, i32]),
+        "lrs_ista_f32": (i32, [vp, vp, vp, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp, vp, sz, vp]),
+        "lrs_ista_set_rs_cols": (i32, [i32]),
+        "lrs_nlm_matlab_col_f32": (i32, [vp, i64, vp, i64, i64, i64, f64, vp, vp]),
         "lrs_ssim_f32": (i32, [vp, vp, i32, i32, i32, vp, vp]),
         "lrs_psnr_workspace": (sz, [i64, i64]),
         "lrs_psnr_bands_f32": (i32, [vp, vp, i64, i64, vp, vp, sz, vp]),

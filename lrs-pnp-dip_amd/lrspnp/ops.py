@@ -14,7 +14,7 @@ from ._lib import (ALPHA_FRO4, ALPHA_SOFT, ALPHA_SPEC2, PROX_NLM, PROX_NLM_MATLA
                    device_lib, lib)
 
 __all__ = ["nlm_col", "block_grid", "cover_ranges", "im2col", "ista_alpha", "ista", "svt_workspace",
-           "svt", "svt_gram", "svt_gram_view", "svt_finish", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT",
+           "ista_workspace", "nlm_matlab_col", "svt", "svt_gram", "svt_gram_view", "svt_finish", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT",
            "PROX_NLM_MATLAB"]
 
 
@@ -117,9 +117,17 @@ def ista_alpha(D, obs_pat, n: int, mode: int, lambda_ista: float, stream=None):
     return alpha, thr
 
 
+def ista_workspace(n: int, K: int, prox: int, device) -> torch.Tensor | None:
+    """Device workspace of lrs_ista_f32 (the row-split kernel's fragment-ordered dictionary images);
+    None when the dictionary-resident kernels serve (n <= 64, K = 256, skimage / soft prox)."""
+    nbytes = int(lib().lrs_ista_workspace(int(n), int(K), int(prox)))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device) if nbytes else None
+
+
 def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=None, coefs=None,
-         want_coefs=False, stream=None):
-    """Masked ISTA + prox over all blocks; returns phi (nb, n_pad) [, coefs (nb, K)]."""
+         want_coefs=False, ws=None, stream=None):
+    """Masked ISTA + prox over all blocks; returns phi (nb, n_pad) [, coefs (nb, K)].  `ws`: an
+    ista_workspace() buffer (allocated here when None and needed)."""
     L = device_lib()
     _dev(Yb, torch.float32, "Yb")
     _dev(obs, torch.uint8, "obs")
@@ -132,9 +140,24 @@ def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=Non
         phi = torch.empty((nb, n_pad), dtype=torch.float32, device=Yb.device)
     if want_coefs and coefs is None:
         coefs = torch.empty((nb, K), dtype=torch.float32, device=Yb.device)
+    if ws is None:
+        ws = ista_workspace(n, K, prox, Yb.device)
     check(L.lrs_ista_f32(_p(Yb), _p(obs), _p(D), n, n_pad, K, nb, _p(alpha), _p(thr), int(Nit), int(prox),
-                         _p(coefs) if want_coefs else None, _p(phi), _s(stream)), "lrs_ista_f32")
+                         _p(coefs) if want_coefs else None, _p(phi), _p(ws), 0 if ws is None else ws.numel(),
+                         _s(stream)), "lrs_ista_f32")
     return (phi, coefs) if want_coefs else phi
+
+
+def nlm_matlab_col(g: torch.Tensor, h, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """NLmeansfilter(g_v, 3, 3, h) (LRS-PnP(Matlab Code)/NLmeansfilter.m) of every row of g (nvec, K)."""
+    L = device_lib()
+    g = _dev(g, torch.float32, "g")
+    g2 = g.view(1, -1) if g.dim() == 1 else g
+    nvec, K = g2.shape
+    o = torch.empty_like(g2) if out is None else _dev(out, torch.float32, "out").view(nvec, K)
+    hv, hs = (_dev(h, torch.float64, "h"), 0.0) if isinstance(h, torch.Tensor) else (None, float(h))
+    check(L.lrs_nlm_matlab_col_f32(_p(g2), K, _p(o), K, K, nvec, hs, _p(hv), _s(stream)), "lrs_nlm_matlab_col_f32")
+    return o.view_as(g)
 
 
 def svt_workspace(P: int, B: int, device) -> torch.Tensor:

@@ -130,6 +130,7 @@ class LrsPnP:
         self.U = torch.empty_like(self.Y)
         self.Yb = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
         self.phi = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
+        self.ista_ws = ops.ista_workspace(n, self.K, self.prox, dev)
         self.norms = torch.zeros(3, dtype=torch.float64, device=dev)
         self.lowrank_stream = torch.cuda.Stream(device=dev)
         self.iteration = 0
@@ -168,7 +169,7 @@ class LrsPnP:
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
                    stream=stream)
         return ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox,
-                        phi=self.phi, want_coefs=want_coefs, stream=stream)
+                        phi=self.phi, want_coefs=want_coefs, ws=self.ista_ws, stream=stream)
 
     def low_rank(self, stream=None, s_out=None):
         warm = self.cfg.svt_warm and self.iteration > 0
@@ -209,7 +210,7 @@ class LrsPnP:
             # its Gram waits for the first sparse-coding workgroups to retire
             main.wait_event(gram_done)
         ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
-                 stream=main)
+                 ws=self.ista_ws, stream=main)
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
                         self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)
@@ -223,7 +224,7 @@ class LrsPnP:
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
                    stream=main)
         ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
-                 stream=main)
+                 ws=self.ista_ws, stream=main)
         self.low_rank_dip(lr)
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,

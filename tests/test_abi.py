@@ -49,5 +49,5 @@ def test_cover_ranges():
 def test_invalid_arguments_rejected():
     L = _lib.lib()
     assert L.lrs_block_count(10, 10, 20, 20) < 0
-    assert L.lrs_ista_f32(None, None, None, 64, 64, 256, 10, None, None, 10, 0, None, None, None) == -1
+    assert L.lrs_ista_f32(None, None, None, 64, 64, 256, 10, None, None, 10, 0, None, None, None, 0, None) == -1
     assert L.lrs_nlm_col_f32(None, 0, None, 0, 0, 0, 0.0, None, 3, 3, None) == -1

@@ -82,16 +82,20 @@ def _rand_blocks(rng, nb, n, miss_frac, scale=0.3):
     return Yb, obs
 
 
-@pytest.mark.parametrize("bb,nb,Nit,variant", [(8, 300, 80, "spec2"), (8, 129, 100, "fro4"),
-                                               (8, 64, 40, "soft"), (36, 20, 12, "fro4"),
-                                               (36, 9, 10, "spec2"), (8, 70, 30, "matlab"),
-                                               (36, 5, 8, "matlab")])
-def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant):
+@pytest.mark.parametrize("bb,nb,Nit,variant,K", [
+    (8, 300, 80, "spec2", 256), (8, 129, 100, "fro4", 256), (8, 64, 40, "soft", 256),
+    (36, 20, 12, "fro4", 256), (36, 9, 10, "spec2", 256), (8, 70, 30, "matlab", 256), (36, 5, 8, "matlab", 256),
+    # row-split kernel: dictionary sizes other than 256 (main_LRS_PnP.py:159-165 loads a trained
+    # dictionary of unknown K), ragged n, many workgroups, every prox
+    (36, 40, 10, "fro4", 128), (36, 17, 10, "fro4", 512), (36, 23, 8, "spec2", 200), (36, 30, 6, "soft", 256),
+    (8, 50, 20, "fro4", 64), (8, 33, 20, "spec2", 100), (8, 20, 15, "soft", 300), (8, 21, 10, "fro4", 7),
+    (20, 37, 10, "fro4", 256), (5, 19, 12, "spec2", 256), (36, 250, 5, "fro4", 256), (36, 3, 100, "fro4", 256)])
+def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant, K):
     from lrspnp.data import synthetic_dictionary
-    rng = np.random.default_rng(bb * 1000 + nb)
+    rng = np.random.default_rng(bb * 1000 + nb + K)
     n = bb * bb
     n_pad = -(-n // 16) * 16
-    D = synthetic_dictionary(n, 256, seed=3)
+    D = synthetic_dictionary(n, K, seed=3)
     Yb, obs = _rand_blocks(rng, nb, n, 0.2)
     alpha = np.empty(nb, np.float32); thr = np.empty(nb, np.float64)
     for j in range(nb):
@@ -291,28 +295,21 @@ def test_ista_both_product_precisions_match_oracle():
     assert rel(out[1][0], out[0][0]) < 1e-6
 
 
-def test_nlm_matlab_prox_bitexact():
-    """The in-register MATLAB-variant prox (NLmeansfilter.m closed form, fp64) against the oracle's
-    C restatement at several h (including h where the exp weights are tiny): same evaluation order,
-    so the only difference is exp() itself (device libm vs glibc, <= 1 fp64 ulp), which flips the
-    float32 rounding of an output in ~1e-4 of the elements: <= 1 float32 ulp."""
-    import ctypes
-    from lrspnp import _lib
-    f = _lib.device_lib().lrs_diag_nlm_matlab
-    vp = ctypes.c_void_p
-    f.argtypes = [vp, vp, ctypes.c_int64, vp, vp]
+def test_nlm_matlab_prox_bitexact(ops):
+    """lrs_nlm_matlab_col_f32 (NLmeansfilter.m closed form, fp64; the prox of the row-split ISTA
+    kernel) against the oracle's C restatement at several h (including h where the exp weights are
+    tiny) and K: same evaluation order, so the only difference is exp() itself (device libm vs glibc,
+    <= 1 fp64 ulp), which flips the float32 rounding of an output in ~1e-4 of the elements."""
     rng = np.random.default_rng(7)
-    nb = 40
-    g = (rng.standard_normal((nb, 256)) * 0.1).astype(np.float32)
-    h = np.geomspace(1e-4, 1.0, nb)
-    gd, hd = torch.from_numpy(g).cuda(), torch.from_numpy(h).cuda()
-    out = torch.empty_like(gd)
-    assert f(vp(gd.data_ptr()), vp(hd.data_ptr()), nb, vp(out.data_ptr()),
-             vp(torch.cuda.current_stream().cuda_stream)) == 0
-    ref = np.stack([O.nlm_matlab_col(g[j], h[j]) for j in range(nb)])
-    o = out.cpu().numpy()
-    np.testing.assert_array_max_ulp(o, ref, maxulp=1)
-    assert np.count_nonzero(o != ref) <= 1e-3 * o.size
+    for K in (256, 100, 7):
+        nb = 40
+        g = (rng.standard_normal((nb, K)) * 0.1).astype(np.float32)
+        h = np.geomspace(1e-4, 1.0, nb)
+        out = ops.nlm_matlab_col(torch.from_numpy(g).cuda(), torch.from_numpy(h).cuda())
+        ref = np.stack([O.nlm_matlab_col(g[j], h[j]) for j in range(nb)])
+        o = out.cpu().numpy()
+        np.testing.assert_array_max_ulp(o, ref, maxulp=1)
+        assert np.count_nonzero(o != ref) <= 1e-3 * o.size + 1
 
 
 def test_compat_pnp_ista_vs_oracle(compat_mod=None):
