@@ -1,32 +1,44 @@
-"""Benchmark: LRS-PnP outer ADMM iterations/sec on the BASELINE.json configs[1] workload.
+"""Benchmark: LRS-PnP-DIP outer ADMM iterations/sec (BASELINE.json `metric`).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cube 200x200x198] [--bb 8] [--nit 80]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload dip|pnp|dip-pro]
 
-One "step" = one outer ADMM iteration of main_LRS_PnP.py (:250-366) over a whole synthetic
-200x200x198 cube: im2col of X + L1/mu1, fused masked ISTA + PnP-NLM prox over all 125,000 8x8
-blocks (Nit = 80, K = 256), SVT low-rank prox (concurrent stream), col2im + X + dual updates.
-Inputs are resident in HBM before the timed region.
+One "step" = one outer ADMM iteration over a whole synthetic cube, inputs resident in HBM:
 
-Multi-GPU (torchrun): one independent cube per rank (seed = rank), no data-path collective
-(weak scaling); barrier + synchronize around the K timed steps, MAX over ranks;
-value = (ranks * K) / max_time.  With --split-cube: ONE cube (seed 0) in pixel-row slabs, one per
-rank, with an fp64 all-reduce of the B x B SVT Gram per iteration (strong scaling, value =
-K / max_time; lrspnp.dist.slab_solver).
+  dip (default, BASELINE configs[2]) — main_LRS_PnP_DIP_1-LiP.py:347-520 on the seeded
+      200x200x198 cube cropped to 196x196x198 (the largest size <= 200 that my_Lipschitz_Unet maps
+      onto itself: 16a-12): im2col of X + L1/mu1, fused masked ISTA + NLM prox
+      over 6,408 36x36 blocks (Nit 100, alpha = 4||H||_F^2), and — concurrently, on a second
+      stream — the DIP low-rank prox: a fresh 1-Lipschitz U-Net (198 -> 128 -> 198 channels)
+      trained for 100 Adam steps (lr 0.1, ES off: SURVEY.md §8d fixes N_dip = 100 for timing),
+      then col2im + closed-form X + dual updates (get_DIP_out :208-264, X update :420-453).
+  pnp (configs[1]) — main_LRS_PnP.py:250-366 on the 200x200x198 cube: 125,000 8x8 blocks,
+      Nit 80, alpha = ||H||_2^2, SVT low-rank prox.
+  dip-pro (configs[3]; with N ranks configs[4]) — main_LRS_PnP_DIP_pro.py on 512x512x224:
+      50,974 36x36 blocks, the skip network DIP.
 
-Rank 0 prints one JSON line, including
-  roofline    : the dominant kernel (lrs_ista_f32 / k_ista_b3) — algorithmic fp32-GEMM FLOPs per
-                launch (Nit*nb*4*n*K + nb*2*n*K) / mean launch time (HIP events on its stream), vs
-                the 157.3 TFLOP/s fp32 MFMA peak (the products are fp32-accurate split-bf16 MFMA;
-                the kernel itself is bound by the fp64 NLM VALU); `traffic` from
-                profiles/ PMC summary when present;
-  cpu_baseline: the oracle (C restatement + numpy alpha/SVT, OpenMP) timed on a bounded sample
-                of the same workload on this host (N = 1, rank 0 only).
+Multi-GPU (one process per GPU, RCCL): one independent cube per rank (seed = rank), no data-path
+collective; barrier + synchronize around the K timed steps, MAX over ranks;
+value = ranks * K / max_time ("weak").  `--gpus N` without a torchrun environment starts N ranks
+itself (a child torch.distributed.run, before any GPU call); a rank count that differs from
+--gpus is an error.  pnp only: --split-cube runs ONE cube over the ranks in pixel-row slabs with an
+fp64 all-reduce of the B x B SVT Gram per iteration ("strong").
+
+Rank 0 prints one JSON line with
+  roofline     : the dominant stage — the DIP training of one outer iteration (dip workloads) or
+                 the ISTA kernel (pnp): algorithmic MFMA FLOPs / time from HIP events on the stream
+                 it runs on, vs the 157.3 TFLOP/s f32 MFMA peak; `traffic` = HBM bytes from the
+                 committed rocprofv3 PMC pass (profiles/r02/traffic.json), per the same unit.
+                 `roofline.kernels` adds the sparse-coding kernel (k_ista_rs / k_ista_ln2) per launch.
+  cpu_baseline : the oracle timed on this host (rank 0, N = 1): the C ISTA restatement on a bounded
+                 block sample + (dip) the plain-torch DIP restatement (oracle/dip_ref.py) for a few
+                 steps, both extrapolated to a full outer iteration, + the full ADMM update.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -38,31 +50,53 @@ for _p in (REPO, os.path.join(REPO, "lrs-pnp-dip_amd")):
 import numpy as np  # noqa: E402
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
-FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table
-HBM_PEAK_GBS = 8000.0
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table (f32 MFMA = f32 vector peak)
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02", "traffic.json")
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cube", default="200x200x198")
-    ap.add_argument("--bb", type=int, default=8)
-    ap.add_argument("--nit", type=int, default=80)
+    ap.add_argument("--steps", type=int, default=None, help="timed outer iterations (default 3 dip, 10 pnp)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed outer iterations (default 1 dip, 2 pnp)")
+    ap.add_argument("--workload", default="dip", choices=["dip", "pnp", "dip-pro"])
+    ap.add_argument("--cube", default=None, help="HxWxB (default: the workload's cube)")
+    ap.add_argument("--bb", type=int, default=None)
+    ap.add_argument("--nit", type=int, default=None)
     ap.add_argument("--K", type=int, default=256)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--dip-steps", type=int, default=100, help="DIP steps per outer iteration (ES off, §8d)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group: nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--split-cube", action="store_true",
-                    help="one cube over all ranks in pixel-row slabs (strong scaling; SVT Gram all-reduce)")
-    ap.add_argument("--workload", default="pnp", choices=["pnp", "dip", "dip-pro"],
-                    help="pnp: BASELINE configs[1] (the headline); dip: configs[2], LRS-PnP-DIP(1-Lip) on a "
-                         "196x196x198 cube (the 200x200 cube cropped to a size the U-Net maps onto itself); "
-                         "dip-pro: configs[3], LRS-PnP-DIP with the skip net on a 512x512x224 cube")
-    ap.add_argument("--dip-steps", type=int, default=100, help="DIP steps per outer iteration (ES off, §8d)")
-    return ap.parse_args()
+                    help="pnp only: one cube over all ranks in pixel-row slabs (strong scaling)")
+    a = ap.parse_args()
+    dip = a.workload != "pnp"
+    if a.steps is None:
+        a.steps = 3 if dip else 10
+    if a.warmup is None:
+        a.warmup = 1 if dip else 2
+    if a.split_cube and dip:
+        ap.error("--split-cube applies to --workload pnp only (the DIP trains on the whole image)")
+    return a
+
+
+def ensure_ranks(args):
+    """--gpus N: under torchrun the world size must equal N; without a torchrun environment,
+    N > 1 re-launches this script under torch.distributed.run as a CHILD process (nothing has
+    touched the GPU yet) and exits with its code."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus <= 1:
+            return
+        port = os.environ.get("MASTER_PORT", str(29500 + (os.getpid() % 1000)))
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", port, os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    if int(world) != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}\n")
+        sys.exit(2)
 
 
 def make_problem(H, W, B, bb, K, seed):
@@ -72,55 +106,137 @@ def make_problem(H, W, B, bb, K, seed):
     return unfold(obs), mask_matrix(mask, B), synthetic_dictionary(bb * bb, K, 0), clean
 
 
-def cpu_baseline(Y, M, D, bb, nit, budget_s):
-    """Oracle timed on a bounded sample of the same workload (host cores)."""
+def load_traffic(key):
+    try:
+        return json.load(open(TRAFFIC_FILE)).get(key)
+    except Exception:
+        return None
+
+
+class StreamTimer:
+    """HIP events around a call, on the stream the call's kernels are launched on."""
+
+    def __init__(self):
+        self.ev = []
+        self.on = False
+
+    def wrap(self, fn, stream_of):
+        import torch
+
+        def timed(*a, **k):
+            st = stream_of(a, k)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            out = fn(*a, **k)
+            e1.record(st)
+            if self.on:
+                self.ev.append((e0, e1))
+            return out
+        return timed
+
+    def mean_ms(self):
+        return float(np.mean([a.elapsed_time(b) for a, b in self.ev])) if self.ev else float("nan")
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline (oracle), rank 0 at N = 1 only
+# ------------------------------------------------------------------------------------------------
+def _threads():
+    t = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(t)
+    return t
+
+
+def cpu_sparse_coding(Y, D, bb, nit, variant, budget_s):
+    """Seconds per outer iteration of the oracle's sparse coding (alpha per block as the reference
+    computes it inside ista(), + the C ISTA), from a growing random block sample."""
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    os.environ["OMP_NUM_THREADS"] = str(threads)
     P, B = Y.shape
     rows, cols = O.block_grid(P, B, bb, bb)
     nb = rows.size
     rng = np.random.default_rng(0)
-    # per-block cost: alpha (numpy float32 SVD of the pruned dictionary, as ista() does per call)
-    # + the C ISTA (GEMVs + NLM) — grow the sample until the budget is used
     blocks = O.im2col(Y, bb, rows, cols)
     obs = (blocks != 0).astype(np.uint8)
-    done, t_ista, t_alpha = 0, 0.0, 0.0
-    batch = 256
+    done, t_alpha, t_ista, batch = 0, 0.0, 0.0, 64 if bb > 8 else 256
     t_start = time.perf_counter()
-    while time.perf_counter() - t_start < budget_s * 0.7 and done < nb:
+    while (time.perf_counter() - t_start < budget_s or done == 0) and done < nb:
         idx = rng.choice(nb, batch, replace=False)
         t0 = time.perf_counter()
         al = np.empty(batch, np.float32)
         th = np.empty(batch, np.float64)
         for k, j in enumerate(idx):
-            al[k], th[k] = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, "spec2")
+            al[k], th[k] = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, variant)
         t1 = time.perf_counter()
         O.ista_batch(blocks[idx], obs[idx], D, al, th, nit)
-        t2 = time.perf_counter()
+        t_ista += time.perf_counter() - t1
         t_alpha += t1 - t0
-        t_ista += t2 - t1
         done += batch
-    per_block = (t_alpha + t_ista) / done
-    t0 = time.perf_counter()
-    U = O.svt(Y, 1 / 0.9)                                   # the reference's float32 LAPACK SVT
-    t_svt = time.perf_counter() - t0
+    return (t_alpha + t_ista) / done * nb, done, nb, t_alpha / done * nb
+
+
+def cpu_admm(Y, M, bb):
+    from oracle import oracle as O
+    P, B = Y.shape
+    rows, cols = O.block_grid(P, B, bb, bb)
+    nb = rows.size
     X = Y.copy()
     PHI = np.zeros((nb, bb * bb), np.float32)
     t0 = time.perf_counter()
-    O.lib().oracle_admm_update(P, B, bb, nb, rows, cols, PHI, Y, M, U, X, X, 0.5, np.float32(0.15),
+    O.lib().oracle_admm_update(P, B, bb, nb, rows, cols, PHI, Y, M, Y, X, X, 0.5, np.float32(0.15),
                                np.float32(0.9), X.copy(), X.copy(), X.copy(), None, None)
-    t_admm = time.perf_counter() - t0
-    t_iter = per_block * nb + t_svt + t_admm
+    return time.perf_counter() - t0
+
+
+def cpu_baseline_pnp(Y, M, D, bb, nit, budget_s):
+    from oracle import oracle as O
+    threads = _threads()
+    t_sc, done, nb, t_alpha = cpu_sparse_coding(Y, D, bb, nit, "spec2", budget_s * 0.7)
+    t0 = time.perf_counter()
+    O.svt(Y, 1 / 0.9)                                       # the reference's float32 LAPACK SVT
+    t_svt = time.perf_counter() - t0
+    t_admm = cpu_admm(Y, M, bb)
+    t_iter = t_sc + t_svt + t_admm
     return {"value": 1.0 / t_iter, "unit": "outer_iters/s", "cores": threads, "kind": "port",
-            "sample": f"{done} of {nb} blocks (alpha+ISTA, Nit={nit}) extrapolated x{nb / done:.1f}, "
-                      f"+ full SVT ({t_svt:.2f}s) + full ADMM update ({t_admm:.3f}s); "
-                      f"est. {t_iter:.1f}s per outer iteration"}
+            "sample": f"{done} of {nb} blocks (alpha+ISTA, Nit={nit}) extrapolated x{nb / done:.1f} "
+                      f"({t_sc:.1f}s, of which per-block alpha {t_alpha:.1f}s), + full SVT ({t_svt:.2f}s) + "
+                      f"full ADMM update ({t_admm:.3f}s); est. {t_iter:.1f}s per outer iteration"}
 
 
+def cpu_baseline_dip(solver, Y, M, D, bb, nit, dip_steps, budget_s):
+    import torch
+
+    from oracle import dip_ref
+    threads = _threads()
+    torch.set_num_threads(threads)
+    t_sc, done, nb, t_alpha = cpu_sparse_coding(Y, D, bb, nit, "fro4", budget_s * 0.4)
+    net = solver.dip.net
+    x = solver.dip_in.detach().cpu()
+    target = solver.dip_target.detach().cpu()
+    mask = solver.dip_mask.detach().cpu()
+    tr = dip_ref.RefTrainer(net.nodes, net.params.detach().cpu())
+    tr.step(x, target, mask)                                # warm (allocator, thread pool)
+    steps, t_dip = 0, 0.0
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < budget_s * 0.5 or steps == 0:
+        t0 = time.perf_counter()
+        tr.step(x, target, mask)
+        t_dip += time.perf_counter() - t0
+        steps += 1
+    per_step = t_dip / steps
+    t_admm = cpu_admm(Y, M, bb)
+    t_iter = t_sc + per_step * dip_steps + t_admm
+    return {"value": 1.0 / t_iter, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+            "sample": f"sparse coding: {done} of {nb} blocks (alpha+ISTA, Nit={nit}, oracle C) extrapolated "
+                      f"x{nb / done:.1f} = {t_sc:.1f}s; DIP: {steps} training steps of the torch-CPU restatement "
+                      f"(oracle/dip_ref.py: conv/BN/LeakyReLU, full-SVD sigma_max per conv, Adam) at "
+                      f"{per_step:.2f}s/step x {dip_steps} = {per_step * dip_steps:.1f}s; full ADMM update "
+                      f"{t_admm:.3f}s; est. {t_iter:.1f}s per outer iteration"}
+
+
+# ------------------------------------------------------------------------------------------------
 def dip_flops_per_step(net):
-    """Algorithmic MFMA FLOPs of one DIP training step of a DipNet: conv forward + dW + dX (no dX
-    for a conv reading the network input)."""
+    """Algorithmic MFMA FLOPs of one DIP training step: conv forward + dW + dX (no dX for a conv
+    that reads the network input)."""
     sh = [net.in_shape] + list(net.shapes)
     tot = 0
     for i, nd in enumerate(net.nodes):
@@ -132,86 +248,95 @@ def dip_flops_per_step(net):
     return tot
 
 
-def main_dip(args):
+def ista_entry(name, ista_ms, flops, traffic_key):
+    achieved = flops / (ista_ms * 1e-3) / 1e12
+    return {"kernel": name, "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": load_traffic(traffic_key),
+            "flops_per_launch": flops, "ms_per_launch": ista_ms}
+
+
+def main_dip(args, ctx):
     import torch
 
-    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp import LrsPnP, LrsPnPConfig, ops
     from lrspnp import dist as D
     from lrspnp.dip import DipConfig
     from lrspnp.metrics import mpsnr
-    ctx = D.init_from_env(args.backend)
     pro = args.workload == "dip-pro"
-    H = W = 512 if pro else 196
-    B = 224 if pro else 198
-    bb = 36 if args.bb == 8 else args.bb
+    H, W, B = (int(v) for v in args.cube.split("x")) if args.cube else ((512, 512, 224) if pro else (196, 196, 198))
+    bb = args.bb or 36
+    nit = args.nit or 100
     Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=ctx.rank)
     dcfg = DipConfig(num_iter=args.dip_steps, early_stop=False, net="skip" if pro else "unet1lip")
-    cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, dip=dcfg)
+    cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, Nit=nit, dip=dcfg)
     s = LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
     clean_d = torch.from_numpy(clean).cuda()
     mp0 = mpsnr(s.X, clean_d)
-    # DIP training time per outer iteration: events on the low-rank stream around the DIP call
-    ev = []
-    orig = s.low_rank_dip
 
-    def timed(stream):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        orig(stream)
-        e1.record(stream)
-        ev.append((e0, e1))
+    dip_t, ista_t = StreamTimer(), StreamTimer()
+    s.low_rank_dip = dip_t.wrap(s.low_rank_dip, lambda a, k: a[0])
+    orig_ista = ops.ista
+    ops.ista = ista_t.wrap(orig_ista, lambda a, k: k.get("stream") or torch.cuda.current_stream())
+    count = [0]
 
-    s.low_rank_dip = timed
-    elapsed = D.timed_steps(s.step, args.steps, args.warmup, ctx)
-    dip_ms = float(np.mean([a.elapsed_time(b) for a, b in ev[args.warmup:]]))
+    def step():
+        dip_t.on = ista_t.on = count[0] >= args.warmup
+        count[0] += 1
+        s.step()
+
+    elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
+    ops.ista = orig_ista
     mp1 = mpsnr(s.X, clean_d)
+    dip_ms, ista_ms = dip_t.mean_ms(), ista_t.mean_ms()
     flops = dip_flops_per_step(s.dip.net) * args.dip_steps
     achieved = flops / (dip_ms * 1e-3) / 1e12
+    n = bb * bb
+    ista_flops = nit * s.nb * 4 * n * args.K + s.nb * 2 * n * args.K
+    net_desc = ("skip net (5 x 128 ch, 128-ch skips)" if pro else f"my_Lipschitz_Unet ({B}->128->{B} ch)")
+    tag = "dip_pro" if pro else "dip"
     out = {
         "metric": METRIC, "value": ctx.world * args.steps / elapsed, "unit": "outer_iters/s",
         "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32 (MFMA) + f64 (NLM, BN/sigma statistics)",
-        "data": f"synthetic (seeded low-rank {H}x{W}x{B} cube per rank, random-init DIP net per outer iteration)",
-        "config": {"workload": (f"LRS-PnP-DIP(pro) {H}x{W}x{B}, {bb}x{bb} blocks, K={args.K}, Nit=100 fro4 ISTA, "
-                                f"DIP skip net (5x128 ch, 128 skips) {args.dip_steps} Adam steps, ES off "
-                                "(BASELINE configs[3])") if pro else
-                               (f"LRS-PnP-DIP(1-Lip) 196x196x198, {bb}x{bb} blocks, K={args.K}, Nit=100 fro4 ISTA, "
-                                f"DIP my_Lipschitz_Unet (198->128->198 ch) {args.dip_steps} Adam steps, ES off "
-                                "(BASELINE configs[2])"), "blocks": s.nb,
-                   "parallelism": f"{ctx.world} independent cube(s), one per GPU"},
-        "roofline": {"bound": "mfma", "kernel": "DIP training (conv GEMMs + BN/sigma/Adam kernels)",
+        "vs_baseline": None, "dtype": "f32 (MFMA products fp32-accurate) + f64 (NLM prox, BN/sigma statistics)",
+        "data": f"synthetic (seeded low-rank {H}x{W}x{B} cube per rank, tiled low_rank_sparsity_mask, seeded "
+                f"K={args.K} dictionary, random-init DIP net per outer iteration)",
+        "config": {"workload": (f"LRS-PnP-DIP(pro) {H}x{W}x{B} (BASELINE configs[3]; configs[4] = one such cube per "
+                                f"GPU)" if pro else
+                                f"LRS-PnP-DIP(1-Lip) on the 200x200x198 cube cropped to {H}x{W}x{B} "
+                                f"(BASELINE configs[2]; 196 = largest 16a-12 size <= 200 that the U-Net maps onto "
+                                f"itself)") + f": {bb}x{bb} blocks ({s.nb}), K={args.K}, Nit={nit} fro4 ISTA + NLM "
+                               f"prox; DIP {net_desc} {args.dip_steps} Adam steps per outer iteration, ES off",
+                   "blocks": s.nb, "parallelism": f"{ctx.world} independent cube(s), one per GPU"},
+        "roofline": {"bound": "mfma", "kernel": f"DIP training of one outer iteration ({args.dip_steps} steps: conv "
+                                                f"GEMMs, sigma_max, BN, loss, Adam kernels)",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                     "flops_per_outer_iter": flops, "dip_ms_per_outer_iter": dip_ms},
-        "mpsnr": {"input": mp0, "after_steps": mp1, "steps_run": args.warmup + args.steps},
+                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                     "traffic": load_traffic(f"{tag}_hbm_bytes_per_outer_iter"),
+                     "flops_per_outer_iter": flops, "ms_per_outer_iter": dip_ms,
+                     "kernels": [ista_entry(f"k_ista_rs (lrs_ista_f32: {s.nb} blocks of {n} rows, Nit {nit})",
+                                            ista_ms, ista_flops, f"{tag}_ista_hbm_bytes_per_launch")]},
+        "mpsnr": {"input": mp0, "after_steps": mp1, "outer_iterations_run": args.warmup + args.steps},
     }
-    if ctx.rank == 0:
-        print(json.dumps(out), flush=True)
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_dip(s, Y, M, Dct, bb, nit, args.dip_steps, args.cpu_seconds)
+    return out
 
 
-def main():
-    args = parse()
-    if args.workload in ("dip", "dip-pro"):
-        return main_dip(args)
+def main_pnp(args, ctx):
     import torch
 
-    from lrspnp import dist as D
-    ctx = D.init_from_env(args.backend)
     from lrspnp import LrsPnP, LrsPnPConfig, ops
+    from lrspnp import dist as D
     from lrspnp.metrics import mpsnr
-
-    H, W, B = (int(v) for v in args.cube.split("x"))
+    H, W, B = (int(v) for v in (args.cube or "200x200x198").split("x"))
+    bb = args.bb or 8
+    nit = args.nit or 80
     split = args.split_cube
-    # one cube per rank (seed = rank), or with --split-cube one cube (seed 0) in row slabs
-    Y, M, Dct, clean = make_problem(H, W, B, args.bb, args.K, seed=0 if split else ctx.rank)
-    cfg = LrsPnPConfig(bb=args.bb, sliding=args.bb, Nit=args.nit, variant="spec2")
+    Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=0 if split else ctx.rank)
+    cfg = LrsPnPConfig(bb=bb, sliding=bb, Nit=nit, variant="spec2")
     t0 = time.perf_counter()
-    if split:
-        s, _ = D.slab_solver(Y, M, Dct, cfg, ctx)
-    else:
-        s = LrsPnP(Y, M, Dct, cfg)
+    s = D.slab_solver(Y, M, Dct, cfg, ctx)[0] if split else LrsPnP(Y, M, Dct, cfg)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
     clean_d = torch.from_numpy(clean).cuda()
@@ -223,80 +348,67 @@ def main():
         return mpsnr(torch.from_numpy(X).cuda(), clean_d) if X is not None else float("nan")
 
     mp0 = cube_mpsnr()
-
-    # dominant-kernel timing: HIP events on the stream the ISTA kernel is launched on
-    ev = []
+    ista_t = StreamTimer()
     orig_ista = ops.ista
-    timing = [False]
-
-    def timed_ista(*a, **k):
-        st = k.get("stream") or torch.cuda.current_stream()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        out = orig_ista(*a, **k)
-        e1.record(st)
-        if timing[0]:
-            ev.append((e0, e1))
-        return out
-
-    ops.ista = timed_ista
+    ops.ista = ista_t.wrap(orig_ista, lambda a, k: k.get("stream") or torch.cuda.current_stream())
+    count = [0]
+    track = []
 
     def step():
-        if not timing[0] and warm_done[0] >= args.warmup:
-            timing[0] = True
-        warm_done[0] += 1
+        ista_t.on = count[0] >= args.warmup
+        count[0] += 1
         s.step()
+        if count[0] <= min(2, args.warmup) and not split:
+            track.append(mpsnr(s.X, clean_d))      # the first two iterates, for the oracle fixture below
 
-    warm_done = [0]
     elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
     ops.ista = orig_ista
-    ista_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     mp1 = cube_mpsnr()
     world, rank = ctx.world, ctx.rank
-    mps = [[mp0, mp1]] if split else D.gather_scalars([mp0, mp1], ctx)   # split: one cube, MPSNR on rank 0
-
-    n, K, nb = args.bb * args.bb, args.K, s.nb
-    flops = args.nit * nb * 4 * n * K + nb * 2 * n * K
-    achieved = flops / (ista_ms * 1e-3) / 1e12
-    traffic = None
-    prof = os.path.join(REPO, "profiles", "ista_pmc_traffic.json")
-    if os.path.exists(prof):
-        try:
-            traffic = json.load(open(prof)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    mps = [[mp0, mp1]] if split else D.gather_scalars([mp0, mp1], ctx)
+    n, K = bb * bb, args.K
+    flops = nit * s.nb * 4 * n * K + s.nb * 2 * n * K
+    entry = ista_entry("k_ista_ln2 (lrs_ista_f32)", ista_t.mean_ms(), flops, "pnp_ista_hbm_bytes_per_launch")
+    roof = {k: entry[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+                                  "flops_per_launch", "ms_per_launch")}
     out = {
-        "metric": METRIC,
-        "value": (1 if split else world) * args.steps / elapsed,
-        "unit": "outer_iters/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "strong" if split else "weak",
-        "vs_baseline": None,
-        "dtype": "f32 (MFMA) + f64 (NLM prox, Gram/eig)",
+        "metric": METRIC, "value": (1 if split else world) * args.steps / elapsed, "unit": "outer_iters/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong" if split else "weak", "vs_baseline": None,
+        "dtype": "f32 (MFMA products fp32-accurate) + f64 (NLM prox, Gram/eig)",
         "data": "synthetic (seeded low-rank cube per rank, tiled low_rank_sparsity_mask, seeded K=256 dictionary)",
-        "config": {"workload": f"LRS-PnP (no DIP) {args.cube} cube, {args.bb}x{args.bb} blocks, K={K}, "
-                               f"Nit={args.nit} inner ISTA, SVT low-rank prox (BASELINE configs[1])",
-                   "blocks": int(ops.block_grid(Y.shape[0], B, args.bb, args.bb)[0].size),
+        "config": {"workload": f"LRS-PnP (no DIP) {H}x{W}x{B} cube, {bb}x{bb} blocks, K={K}, Nit={nit} inner ISTA, "
+                               f"SVT low-rank prox (BASELINE configs[1])",
+                   "blocks": s.nb,
                    "parallelism": (f"1 cube in {world} pixel-row slab(s), fp64 Gram all-reduce per iteration"
                                    if split else f"{world} independent cube(s), one per GPU")},
-        "roofline": {"bound": "mfma", "kernel": "k_ista_ln2 (lrs_ista_f32)", "achieved": achieved,
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                     "traffic": traffic, "flops_per_launch": flops, "ms_per_launch": ista_ms},
-        "setup_s": setup_s,
-        "mpsnr": {"input": mp0, "after_steps": mp1, "steps_run": args.warmup + args.steps,
+        "roofline": roof, "setup_s": setup_s,
+        "mpsnr": {"input": mp0, "after_steps": mp1, "outer_iterations_run": args.warmup + args.steps,
                   "per_rank": mps},
     }
+    fx = os.path.join(REPO, "tests", "golden", "cube200_oracle_2iter.npz")
+    if track and (H, W, B, bb, nit, K) == (200, 200, 198, 8, 80, 256) and os.path.exists(fx):
+        with np.load(fx, allow_pickle=False) as z:
+            out["mpsnr"]["first_two_iterates"] = {"gpu": track[:2], "oracle": [float(v) for v in z["mpsnr"]],
+                                                  "oracle_input": float(z["mpsnr_input"])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(Y, M, Dct, args.bb, args.nit, args.cpu_seconds)
-    if rank == 0:
+        out["cpu_baseline"] = cpu_baseline_pnp(Y, M, Dct, bb, nit, args.cpu_seconds)
+    return out
+
+
+def main():
+    args = parse()
+    ensure_ranks(args)
+    from lrspnp import dist as D
+    ctx = D.init_from_env(args.backend)
+    out = main_pnp(args, ctx) if args.workload == "pnp" else main_dip(args, ctx)
+    if out["n_gpus"] != args.gpus:
+        raise SystemExit(f"bench.py: ran on {out['n_gpus']} rank(s), --gpus {args.gpus}")
+    if ctx.rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if ctx.world > 1:
         import torch.distributed as tdist
+        tdist.barrier()
         tdist.destroy_process_group()
 
 

@@ -32,6 +32,7 @@
 
 namespace lrs {
 
+
 struct IstaRsParams {
     const float *Yb;       // [nb][n_pad]
     const uint8_t *obs;    // [nb][n_pad]
@@ -63,11 +64,13 @@ __device__ __forceinline__ int symmetric_idx(int i, int K) {
 }
 
 // skimage 0.18.3 fast NLM of atoms a0..a0+3 of one gradient row in LDS
-__device__ __forceinline__ void prox_nlm_chunk(const float *row, int a0, int K, double kneg, double c0, double seven,
-                                               float (&out)[4]) {
+__device__ __forceinline__ int gsw(int b, int a);
+
+__device__ __forceinline__ void prox_nlm_chunk(const float *row, int b, int a0, int K, double kneg, double c0,
+                                               double seven, float (&out)[4]) {
     double w[11];
 #pragma unroll
-    for (int k = 0; k < 11; ++k) w[k] = (double)row[reflect_idx(a0 - 3 + k, K)];
+    for (int k = 0; k < 11; ++k) w[k] = (double)row[gsw(b, reflect_idx(a0 - 3 + k, K))];
     int W1[7], W2[7], W3[7];
     nlm_weights<true>(w, kneg, W1, W2, W3);
     nlm_outputs<2>(w, W1, W2, W3, c0, seven, out);
@@ -75,13 +78,13 @@ __device__ __forceinline__ void prox_nlm_chunk(const float *row, int a0, int K, 
 
 // NLmeansfilter(g, 3, 3, h) of LRS-PnP(Matlab Code)/NLmeansfilter.m:18-78, one output, fp64, in the
 // evaluation order of oracle/nlm_oracle.c:oracle_nlm_matlab_col
-__device__ __forceinline__ float prox_nlm_matlab_point(const float *row, int i, int K, const double (&krow)[7],
-                                                       double h2) {
+__device__ __forceinline__ float prox_nlm_matlab_point(const float *row, int b, int i, int K,
+                                                       const double (&krow)[7], double h2) {
     double v[13];   // g-hat[i-6 .. i+6]
 #pragma unroll
     for (int k = 0; k < 13; ++k) {
         const int j = i - 6 + k;
-        v[k] = (j >= -3 && j < K + 3) ? (double)row[symmetric_idx(j, K)] : 0.0;
+        v[k] = (j >= -3 && j < K + 3) ? (double)row[gsw(b, symmetric_idx(j, K))] : 0.0;
     }
     double sw = 0.0, av = 0.0, wmax = 0.0;
 #pragma unroll
@@ -101,7 +104,7 @@ __device__ __forceinline__ float prox_nlm_matlab_point(const float *row, int i, 
     }
     av = av + wmax * v[6];
     sw = sw + wmax;
-    return sw > 0.0 ? (float)(av / sw) : row[i];
+    return sw > 0.0 ? (float)(av / sw) : row[gsw(b, i)];
 }
 
 __device__ __forceinline__ void nlm_matlab_krow_d(double (&krow)[7]) {
@@ -122,50 +125,44 @@ __device__ __forceinline__ float rs_div(float a, float b, float y) {
     return __fmaf_rn(r, y, q);
 }
 
-// LDS bytes of one workgroup: max(S-1, 1) partial G images of the C*NQ atom tiles (the last one
-// doubles as the published x) + the gradient rows
-__host__ __device__ constexpr int rs_gstride(int NQ) { return NQ * 16 + 8; }
-__host__ __device__ constexpr size_t rs_lds_bytes(int NQ, int C, int S) {
-    return (size_t)(S > 1 ? S - 1 : 1) * C * NQ * 1024 + (size_t)C * 16 * rs_gstride(NQ) * 4;
-}
+// LDS of one workgroup (floatx4 = 16 B units of [tile][lane]):
+//   part  [NQ atom tiles][S-1 partial G images][64]     (S = 1: none)
+//   xbuf  [NQ][64]            the coefficients x: B operand of every R_t, rewritten by the prox
+//   gbuf  [16 blocks][NQ*16]  the gradient rows read by the prox (chunk index XOR-swizzled by block)
+__host__ __device__ constexpr size_t rs_lds_bytes(int NQ, int S) { return (size_t)(S + 1) * NQ * 1024; }
 
-template <int NQ, int C, int MINW>
+__device__ __forceinline__ int gsw(int b, int a) { return a ^ ((b & 15) << 2); }
+
+// The observation term is split off the residual: D^T (m .* (y - D x)) = b - D^T (m .* D x) with
+// b = D^T (m .* y) formed once per launch (each owner keeps its atom tiles of b in VGPRs), so the
+// inner iterations never re-read y: per row tile they need D (L2), x (LDS) and 4 mask bits (VGPR).
+template <int NQ, int MINW, int S>
 __global__ __launch_bounds__(256, MINW) void k_ista_rs(IstaRsParams p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    constexpr int NTILE = C * NQ;
-    constexpr int KS = rs_gstride(NQ);
+    constexpr int KP = NQ * 16;
     constexpr int RING = 8;
-    const int lane = threadIdx.x & 63, S = blockDim.x >> 6;
+    constexpr int NOWN = (NQ + S - 1) / S;       // atom tiles owned per wave (at most)
+    constexpr int NMW = 4;                       // mask words: 8 row tiles each, in VGPRs
+    const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: row range in SGPRs
     const int jl = lane & 15, g = lane >> 4;
-    floatx4 *part = reinterpret_cast<floatx4 *>(smem);                 // [NTILE][S-1][64]
-    float *gbuf = smem + (size_t)NTILE * (S > 1 ? S - 1 : 1) * 256;  // [C*16][KS]
-    floatx4 *xbuf = part;                                              // [NTILE][64], aliases part
+    floatx4 *part = reinterpret_cast<floatx4 *>(smem);                         // [NQ][S-1][64]
+    floatx4 *xbuf = part + (size_t)(S - 1) * NQ * 64;                          // [NQ][64]
+    float *gbuf = reinterpret_cast<float *>(xbuf + NQ * 64);                   // [16][KP]
     const int NT = p.n_pad >> 4;
     const int t0 = (NT * w) / S, t1 = (NT * (w + 1)) / S;
     const int K = p.K;
 
-    int64_t jc[C];
-    bool valid[C];
-    float al[C], ral[C];
-    double th[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        jc[c] = ((int64_t)blockIdx.x * C + c) * 16 + jl;
-        valid[c] = jc[c] < p.nb;
-        al[c] = valid[c] ? p.alpha[jc[c]] : 1.0f;
-        ral[c] = 1.0f / al[c];
-        th[c] = valid[c] ? p.thr[jc[c]] : 1.0;
-    }
+    const int64_t j = (int64_t)blockIdx.x * 16 + jl;
+    const bool valid = j < p.nb;
+    const float al = valid ? p.alpha[j] : 1.0f;
+    const float ral = 1.0f / al;
+    const double th = valid ? p.thr[j] : 1.0;
     const double c0 = nlm_c0();
     double krow[7];
     nlm_matlab_krow_d(krow);
 
-    float X[C][NQ][4];
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) X[c][q][0] = X[c][q][1] = X[c][q][2] = X[c][q][3] = 0.f;
+    for (int i = threadIdx.x; i < NQ * 64; i += 64 * S) xbuf[i] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     // fragment k of row tile t: k < NQ -> DAf q = k, else DTf q = k - NQ.  Buffer loads: the lane's
     // 16-byte offset is the only VGPR, the wave-uniform fragment offset goes in soffset.
@@ -178,184 +175,196 @@ __global__ __launch_bounds__(256, MINW) void k_ista_rs(IstaRsParams p) {
                               : __builtin_amdgcn_raw_buffer_load_b128(rDT, voff, (t * NQ + k - NQ) * 1024, 0);
         return __builtin_bit_cast(float4, v);
     };
+    auto mask4 = [&](int t) -> uint32_t {          // observed-row bits of rows 16t + 4g .. +3
+        const uint32_t mv = valid ? *reinterpret_cast<const uint32_t *>(&p.obs[j * p.n_pad + 16 * t + 4 * g]) : 0u;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bits |= (((mv >> (8 * e)) & 0xffu) ? 1u : 0u) << e;
+        return bits;
+    };
+    auto gq = [&](const floatx4 &G, float4 a, const float (&r)[4]) -> floatx4 {
+        floatx4 acc = G;
+        acc = mfma16x16x4(a.x, r[0], acc);
+        acc = mfma16x16x4(a.y, r[1], acc);
+        acc = mfma16x16x4(a.z, r[2], acc);
+        acc = mfma16x16x4(a.w, r[3], acc);
+        return acc;
+    };
 
-    for (int it = 0; it < p.Nit; ++it) {
-        floatx4 G[C][NQ];
+    // mask bits of this wave's row tiles (tile i: word i / 8, bits 4 (i % 8) .. +3); tiles beyond
+    // 8 NMW per wave re-read theirs
+    uint32_t ms[NMW];
 #pragma unroll
-        for (int c = 0; c < C; ++c)
+    for (int v = 0; v < NMW; ++v) {
+        ms[v] = 0;
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) G[c][q] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < 8; ++u)
+            if (8 * v + u < t1 - t0) ms[v] |= mask4(t0 + 8 * v + u) << (4 * u);
+    }
+    auto mbits = [&](int i) -> uint32_t {
+        if (i >= 8 * NMW) return mask4(t0 + i);
+        const uint32_t word = i < 8 ? ms[0] : i < 16 ? ms[1] : i < 24 ? ms[2] : ms[3];
+        return (word >> (4 * (i & 7))) & 0xfu;
+    };
 
-        float4 ring[RING];
-        if (t0 < t1) {
+    // ---- b = D^T (m .* y): partial over this wave's rows, reduced into the owners' VGPRs ----------
+    floatx4 G[NQ];
 #pragma unroll
-            for (int k = 0; k < RING; ++k) ring[k] = frag(t0, k);
-        }
-        for (int t = t0; t < t1; ++t) {
-            // observations of this row tile (consumed after product A)
-            float4 yv[C];
-            uint32_t mv[C];
+    for (int q = 0; q < NQ; ++q) G[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int t = t0; t < t1; ++t) {
+        const uint32_t m4 = mbits(t - t0);
+        float4 yv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (valid) yv = *reinterpret_cast<const float4 *>(&p.Yb[j * p.n_pad + 16 * t + 4 * g]);
+        const float r[4] = {(m4 & 1u) ? yv.x : 0.f, (m4 & 2u) ? yv.y : 0.f, (m4 & 4u) ? yv.z : 0.f,
+                            (m4 & 8u) ? yv.w : 0.f};
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                yv[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-                mv[c] = 0;
-                if (valid[c]) {
-                    yv[c] = *reinterpret_cast<const float4 *>(&p.Yb[jc[c] * p.n_pad + 16 * t + 4 * g]);
-                    mv[c] = *reinterpret_cast<const uint32_t *>(&p.obs[jc[c] * p.n_pad + 16 * t + 4 * g]);
-                }
-            }
-            floatx4 RA[C], RB[C];
-#pragma unroll
-            for (int c = 0; c < C; ++c) RA[c] = RB[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-            float r[C][4];
-            float4 pend = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int k = 0; k < 2 * NQ; ++k) {
-                const float4 a = ring[k % RING];
-                const int kk = k + RING;
-                if (kk < 2 * NQ) ring[k % RING] = frag(t, kk);
-                else if (t + 1 < t1) ring[k % RING] = frag(t + 1, kk - 2 * NQ);
-                if (k < NQ) {
-                    // R_t += D[rows of t][atoms 16q..] x[16q..]; even / odd q on two accumulators
-#pragma unroll
-                    for (int c = 0; c < C; ++c) {
-                        floatx4 &acc = (k & 1) ? RB[c] : RA[c];
-                        acc = mfma16x16x4(a.x, X[c][k][0], acc);
-                        acc = mfma16x16x4(a.y, X[c][k][1], acc);
-                        acc = mfma16x16x4(a.z, X[c][k][2], acc);
-                        acc = mfma16x16x4(a.w, X[c][k][3], acc);
-                    }
-                    if (k == NQ - 1) {
-#pragma unroll
-                        for (int c = 0; c < C; ++c) {
-                            const floatx4 R = RA[c] + RB[c];
-                            const float y4[4] = {yv[c].x, yv[c].y, yv[c].z, yv[c].w};
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) r[c][e] = ((mv[c] >> (8 * e)) & 0xffu) ? (y4[e] - R[e]) : 0.0f;
-                        }
-                    }
-                } else {
-                    // G_q += D^T[atoms 16q..][rows of t] r_t; q pairs interleaved (MFMA latency)
-                    const int q = k - NQ;
-                    if ((q & 1) == 0) {
-                        pend = a;
-                    } else {
-#pragma unroll
-                        for (int s = 0; s < 4; ++s) {
-                            const float a0 = s == 0 ? pend.x : s == 1 ? pend.y : s == 2 ? pend.z : pend.w;
-                            const float a1 = s == 0 ? a.x : s == 1 ? a.y : s == 2 ? a.z : a.w;
-#pragma unroll
-                            for (int c = 0; c < C; ++c) {
-                                G[c][q - 1] = mfma16x16x4(a0, r[c][s], G[c][q - 1]);
-                                G[c][q] = mfma16x16x4(a1, r[c][s], G[c][q]);
-                            }
-                        }
-                    }
-                }
-            }
-        }
-
-        // ---- reduce the S partial gradients (fixed wave order) and form g = x + G / alpha -------
+        for (int q = 0; q < NQ; ++q) G[q] = gq(G[q], frag(t, NQ + q), r);
+    }
+    auto publish = [&]() {          // partials of the tiles this wave does not own
         if (S > 1) {
 #pragma unroll
-            for (int T = 0; T < NTILE; ++T) {
-                const int o = T % S;
-                if (w != o) part[((size_t)T * (S - 1) + (w - (w > o))) * 64 + lane] = G[T / NQ][T % NQ];
+            for (int q = 0; q < NQ; ++q) {
+                const int o = q % S;
+                if (w != o) part[((size_t)q * (S - 1) + (w - (w > o))) * 64 + lane] = G[q];
             }
-            __syncthreads();
         }
+        __syncthreads();
+    };
+    auto reduced = [&](int q, floatx4 acc) -> floatx4 {   // acc + sum over waves, fixed wave order
 #pragma unroll
-        for (int T = 0; T < NTILE; ++T) {
-            const int c = T / NQ, q = T % NQ;
-            if (w == T % S) {
-                floatx4 s = floatx4{0.f, 0.f, 0.f, 0.f};
-                for (int k = 0; k < S; ++k) {
-                    if (k == w) {
-                        s += G[c][q];
-                    } else {
-                        s += part[((size_t)T * (S - 1) + (k - (k > w))) * 64 + lane];
-                    }
+        for (int k = 0; k < S; ++k) {
+            if (k == w) acc += G[q];
+            else acc += part[((size_t)q * (S - 1) + (k - (k > w))) * 64 + lane];
+        }
+        return acc;
+    };
+    floatx4 bown[NOWN];
+    publish();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+        if (w == q % S) bown[q / S] = reduced(q, floatx4{0.f, 0.f, 0.f, 0.f});
+    __syncthreads();
+
+    // one row tile: R_t = D_t x (x from LDS), r_t = -m .* R_t, G += D_t^T r_t
+    auto row_tile = [&](int t, float4 (&ring)[RING], uint32_t m4) {
+        asm volatile("" ::: "memory");   // x is re-read from LDS per tile, not hoisted into 4 NQ VGPRs
+        floatx4 RA = {0.f, 0.f, 0.f, 0.f}, RB = {0.f, 0.f, 0.f, 0.f};
+        float r[4];
+        float4 pend = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < 2 * NQ; ++k) {
+            const float4 a = ring[k % RING];
+            const int kk = k + RING;
+            if (kk < 2 * NQ) ring[k % RING] = frag(t, kk);
+            else if (t + 1 < t1) ring[k % RING] = frag(t + 1, kk - 2 * NQ);
+            if (k < NQ) {
+                const floatx4 xv = xbuf[k * 64 + lane];
+                floatx4 &acc = (k & 1) ? RB : RA;      // even / odd q on two accumulators (MFMA latency)
+                acc = mfma16x16x4(a.x, xv[0], acc);
+                acc = mfma16x16x4(a.y, xv[1], acc);
+                acc = mfma16x16x4(a.z, xv[2], acc);
+                acc = mfma16x16x4(a.w, xv[3], acc);
+                if (k == NQ - 1) {
+                    const floatx4 R = RA + RB;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) r[e] = ((m4 >> e) & 1u) ? -R[e] : 0.0f;
                 }
+            } else {
+                const int q = k - NQ;             // q pairs interleaved (MFMA latency)
+                if ((q & 1) == 0) {
+                    pend = a;
+                } else {
+                    G[q - 1] = mfma16x16x4(pend.x, r[0], G[q - 1]);
+                    G[q] = mfma16x16x4(a.x, r[0], G[q]);
+                    G[q - 1] = mfma16x16x4(pend.y, r[1], G[q - 1]);
+                    G[q] = mfma16x16x4(a.y, r[1], G[q]);
+                    G[q - 1] = mfma16x16x4(pend.z, r[2], G[q - 1]);
+                    G[q] = mfma16x16x4(a.z, r[2], G[q]);
+                    G[q - 1] = mfma16x16x4(pend.w, r[3], G[q - 1]);
+                    G[q] = mfma16x16x4(a.w, r[3], G[q]);
+                }
+            }
+        }
+    };
+
+    for (int it = 0; it < p.Nit; ++it) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) G[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+        float4 ring[RING];
+#pragma unroll
+        for (int k = 0; k < RING; ++k) ring[k] = frag(t0, k);
+        for (int t = t0; t < t1; ++t) row_tile(t, ring, mbits(t - t0));
+
+        // ---- owner: G = b + sum_w G_w, g = x + G / alpha -> gbuf ----------------------------------
+        publish();
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (w == q % S) {
+                const floatx4 sum = reduced(q, bown[q / S]);
+                const floatx4 xo = xbuf[q * 64 + lane];
                 float4 gr;
-                gr.x = X[c][q][0] + rs_div(s[0], al[c], ral[c]);
-                gr.y = X[c][q][1] + rs_div(s[1], al[c], ral[c]);
-                gr.z = X[c][q][2] + rs_div(s[2], al[c], ral[c]);
-                gr.w = X[c][q][3] + rs_div(s[3], al[c], ral[c]);
-                *reinterpret_cast<float4 *>(&gbuf[(c * 16 + jl) * KS + 16 * q + 4 * g]) = gr;
+                gr.x = xo[0] + rs_div(sum[0], al, ral);
+                gr.y = xo[1] + rs_div(sum[1], al, ral);
+                gr.z = xo[2] + rs_div(sum[2], al, ral);
+                gr.w = xo[3] + rs_div(sum[3], al, ral);
+                *reinterpret_cast<float4 *>(&gbuf[jl * KP + gsw(jl, 16 * q + 4 * g)]) = gr;
             }
         }
         __syncthreads();
 
-        // ---- prox of the owned atom tiles (runtime loop: one inlined prox body), x through LDS ----
-        for (int T = w; T < NTILE; T += S) {
-            const int c = T / NQ, q = T - c * NQ;
-            const double thc = (C == 1 || c == 0) ? th[0] : th[C - 1];
-            const float *row = gbuf + (c * 16 + jl) * KS;
+        // ---- prox of the owned atom tiles (runtime loop: one inlined prox body) -> xbuf ----------
+        for (int q = w; q < NQ; q += S) {
+            const float *row = gbuf + jl * KP;
             const int a0 = 16 * q + 4 * g;
             float o[4];
             if (p.prox == LRS_PROX_SOFT) {
-                const float Tt = (float)thc;
+                const float Tt = (float)th;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const float gv = row[a0 + e];
+                    const float gv = row[gsw(jl, a0 + e)];
                     float tv = fabsf(gv) - Tt;
                     tv = tv > 0.f ? tv : 0.f;
                     o[e] = gv > 0.f ? tv : (gv < 0.f ? -tv : 0.f);
                 }
             } else if (p.prox == LRS_PROX_NLM_MATLAB) {
-                const double h2 = thc * thc;
-                for (int e = 0; e < 4; ++e) o[e] = a0 + e < K ? prox_nlm_matlab_point(row, a0 + e, K, krow, h2) : 0.f;
+                const double h2 = th * th;
+                for (int e = 0; e < 4; ++e)
+                    o[e] = a0 + e < K ? prox_nlm_matlab_point(row, jl, a0 + e, K, krow, h2) : 0.f;
             } else {
-                prox_nlm_chunk(row, a0, K, nlm_kneg(thc), c0, p.seven, o);
+                prox_nlm_chunk(row, jl, a0, K, nlm_kneg(th), c0, p.seven, o);
             }
-            xbuf[(size_t)T * 64 + lane] = floatx4{a0 < K ? o[0] : 0.f, a0 + 1 < K ? o[1] : 0.f, a0 + 2 < K ? o[2] : 0.f,
-                                                  a0 + 3 < K ? o[3] : 0.f};
+            xbuf[q * 64 + lane] = floatx4{a0 < K ? o[0] : 0.f, a0 + 1 < K ? o[1] : 0.f, a0 + 2 < K ? o[2] : 0.f,
+                                          a0 + 3 < K ? o[3] : 0.f};
         }
         __syncthreads();
-#pragma unroll
-        for (int T = 0; T < NTILE; ++T) {
-            const floatx4 v = xbuf[(size_t)T * 64 + lane];
-            X[T / NQ][T % NQ][0] = v[0]; X[T / NQ][T % NQ][1] = v[1];
-            X[T / NQ][T % NQ][2] = v[2]; X[T / NQ][T % NQ][3] = v[3];
-        }
-        __syncthreads();   // the next iteration's partials overwrite xbuf
     }
 
     // ---- outputs: coefficients (owned tiles) and Phi = D x over this wave's row tiles ----------
-    if (p.coefs) {
+    if (p.coefs && valid) {
+        for (int q = w; q < NQ; q += S) {
+            const floatx4 xv = xbuf[q * 64 + lane];
 #pragma unroll
-        for (int T = 0; T < NTILE; ++T) {
-            const int c = T / NQ, q = T % NQ;
-            if (w == T % S && valid[c]) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int a = 16 * q + 4 * g + e;
-                    if (a < K) p.coefs[jc[c] * K + a] = X[c][q][e];
-                }
+            for (int e = 0; e < 4; ++e) {
+                const int a = 16 * q + 4 * g + e;
+                if (a < K) p.coefs[j * K + a] = xv[e];
             }
         }
     }
     for (int t = t0; t < t1; ++t) {
-        floatx4 RA[C], RB[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) RA[c] = RB[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+        floatx4 RA = {0.f, 0.f, 0.f, 0.f}, RB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            const float4 a = p.DAf[((size_t)t * NQ + q) * 64 + lane];
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                floatx4 &acc = (q & 1) ? RB[c] : RA[c];
-                acc = mfma16x16x4(a.x, X[c][q][0], acc);
-                acc = mfma16x16x4(a.y, X[c][q][1], acc);
-                acc = mfma16x16x4(a.z, X[c][q][2], acc);
-                acc = mfma16x16x4(a.w, X[c][q][3], acc);
-            }
+            const float4 a = frag(t, q);
+            const floatx4 xv = xbuf[q * 64 + lane];
+            floatx4 &acc = (q & 1) ? RB : RA;
+            acc = mfma16x16x4(a.x, xv[0], acc);
+            acc = mfma16x16x4(a.y, xv[1], acc);
+            acc = mfma16x16x4(a.z, xv[2], acc);
+            acc = mfma16x16x4(a.w, xv[3], acc);
         }
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            if (!valid[c]) continue;
-            const floatx4 R = RA[c] + RB[c];
-            *reinterpret_cast<float4 *>(&p.phi[jc[c] * p.n_pad + 16 * t + 4 * g]) = make_float4(R[0], R[1], R[2], R[3]);
+        if (valid) {
+            const floatx4 R = RA + RB;
+            *reinterpret_cast<float4 *>(&p.phi[j * p.n_pad + 16 * t + 4 * g]) = make_float4(R[0], R[1], R[2], R[3]);
         }
     }
 }
@@ -393,7 +402,7 @@ __global__ __launch_bounds__(256) void k_nlm_matlab_col(const float *__restrict_
     const double hh = hv ? hv[v] : h;
     double krow[7];
     nlm_matlab_krow_d(krow);
-    for (int i = threadIdx.x; i < K; i += blockDim.x) out[v * ldo + i] = prox_nlm_matlab_point(col, i, K, krow, hh * hh);
+    for (int i = threadIdx.x; i < K; i += blockDim.x) out[v * ldo + i] = prox_nlm_matlab_point(col, 0, i, K, krow, hh * hh);
 }
 
 // ---- launcher ---------------------------------------------------------------------------------
@@ -419,13 +428,14 @@ size_t ista_rs_workspace(int64_t n, int64_t K) {
 }
 
 // Waves per workgroup S: the per-SIMD makespan ceil(tiles S / SIMDs) / S, smallest S on ties;
-// capped by the rows (one row tile per wave at least) and by LDS (two workgroups per CU).
-static int rs_pick_waves(int64_t tiles, int NT, int NQ, int C, int minw) {
+// capped by the rows (one row tile per wave at least) and by LDS (two workgroups per CU at MINW 2);
+// S = 1 only when there is a single row tile (its owner would hold all of b in VGPRs).
+static int rs_pick_waves(int64_t tiles, int NT, int NQ, int minw) {
     const int64_t simds = (int64_t)cu_count() * 4 * (minw >= 2 ? 2 : 1);
-    int best = 1;
+    int best = NT > 1 ? 2 : 1;
     double best_t = 1e30;
-    for (int S = 1; S <= 4 && S <= NT; ++S) {
-        if (rs_lds_bytes(NQ, C, S) > (minw >= 2 ? 81920u : 163840u)) break;
+    for (int S = (NT > 1 ? 2 : 1); S <= 4 && S <= NT; ++S) {
+        if (rs_lds_bytes(NQ, S) > (minw >= 2 ? 81920u : 163840u)) break;
         const double t = (double)((tiles * S + simds - 1) / simds) / S;
         if (t < best_t * 0.999) {
             best_t = t;
@@ -435,22 +445,30 @@ static int rs_pick_waves(int64_t tiles, int NT, int NQ, int C, int minw) {
     return best;
 }
 
-template <int NQ, int C, int MINW>
-static int launch_rs(const IstaRsParams &p, int NT, hipStream_t st) {
-    const int64_t cols = 16 * C;
-    const int64_t tiles = (p.nb + cols - 1) / cols;
-    const int S = rs_pick_waves(tiles, NT, NQ, C, MINW);
-    const size_t lds = rs_lds_bytes(NQ, C, S);
+template <int NQ, int MINW, int S>
+static int launch_rs_k(const IstaRsParams &p, hipStream_t st) {
+    const int64_t tiles = (p.nb + 15) / 16;
     static bool lds_opt_in = false;   // dynamic LDS beyond 64 KiB
     if (!lds_opt_in) {
-        const hipError_t e = hipFuncSetAttribute((const void *)k_ista_rs<NQ, C, MINW>,
+        const hipError_t e = hipFuncSetAttribute((const void *)k_ista_rs<NQ, MINW, S>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return (int)e;
         lds_opt_in = true;
     }
-    hipLaunchKernelGGL((k_ista_rs<NQ, C, MINW>), dim3((unsigned)tiles), dim3(64 * S), lds, st, p);
+    hipLaunchKernelGGL((k_ista_rs<NQ, MINW, S>), dim3((unsigned)tiles), dim3(64 * S), rs_lds_bytes(NQ, S), st, p);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
+}
+
+template <int NQ, int MINW>
+static int launch_rs(const IstaRsParams &p, int NT, hipStream_t st) {
+    const int64_t tiles = (p.nb + 15) / 16;
+    switch (rs_pick_waves(tiles, NT, NQ, MINW)) {
+    case 1: return launch_rs_k<NQ, MINW, 1>(p, st);
+    case 2: return launch_rs_k<NQ, MINW, 2>(p, st);
+    case 3: return launch_rs_k<NQ, MINW, 3>(p, st);
+    default: return launch_rs_k<NQ, MINW, 4>(p, st);
+    }
 }
 
 int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
@@ -470,10 +488,10 @@ int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t 
     }
     IstaRsParams p{Yb, obs, DAf, DTf, alpha, thr, coefs, phi, (int)n_pad, (int)K, Nit, prox, nb, 7.0};
     switch (NQ) {
-    case 4: return launch_rs<4, 1, 2>(p, NT, st);
-    case 8: return launch_rs<8, 1, 2>(p, NT, st);
-    case 16: return cols_per_wave == 2 ? launch_rs<16, 2, 1>(p, NT, st) : launch_rs<16, 1, 2>(p, NT, st);
-    default: return launch_rs<32, 1, 1>(p, NT, st);
+    case 4: return launch_rs<4, 2>(p, NT, st);
+    case 8: return launch_rs<8, 2>(p, NT, st);
+    case 16: return launch_rs<16, 2>(p, NT, st);
+    default: return launch_rs<32, 1>(p, NT, st);
     }
 }
 
