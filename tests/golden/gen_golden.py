@@ -252,6 +252,82 @@ def gen_lrs_pnp_2iter(bridge):
     print("golden MPSNR", mpsnr, file=sys.stderr)
 
 
+def gen_lrs_pnp_cfg0(bridge, iters=50):
+    """BASELINE configs[0] as written: main_LRS_PnP.py for 50 outer iterations on
+    data/low_rank_sparsity_noisy.mat (+ its clean counterpart low_rank_sparsity_clean.mat) with
+    fourth_mask.mat.  The script is executed with two changes made by the harness, not by editing
+    any file: `iteration_num = 2` (main_LRS_PnP.py:231) is set to 50, and its two h5py reads of the
+    img5 files (:170, :177) are served low_rank_sparsity_noisy.mat (a MAT v5 file, read with scipy
+    and handed over in h5py's axis order) and low_rank_sparsity_clean.mat.  Saved: the MPSNR of
+    every iteration, X after iterations 1, 2 and 50, lambda_1 / lambda_2 after 50."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    import scipy.io
+    import torch
+
+    plt.show = lambda *a, **k: None
+    D = synthetic_dictionary(1296, 256, 0)
+    real_loadmat = scipy.io.loadmat
+    served = {"low_rank_sparsity_noisy_img5.mat": "low_rank_sparsity_noisy.mat",
+              "low_rank_sparsity_clean_img5.mat": "low_rank_sparsity_clean.mat"}
+
+    def loadmat(path, *a, **k):
+        if os.path.basename(path) == "trained_dictionary.mat":
+            return {"Dictionary": D.astype(np.float64)}
+        return real_loadmat(os.path.join(REF, "data", os.path.basename(path)), *a, **k)
+
+    class _H5File:
+        def __init__(self, path, mode="r"):
+            self.path = os.path.join(REF, "data", served.get(os.path.basename(path), os.path.basename(path)))
+
+        def __getitem__(self, key):
+            try:
+                v5 = real_loadmat(self.path)[key]                 # (1,128,36,36) in a v5 file
+                return np.ascontiguousarray(np.asarray(v5).transpose(3, 2, 1, 0))
+            except (ValueError, NotImplementedError):
+                return bridge.h5(self.path, key)                  # v7.3 (HDF5)
+
+    fake_h5py = types.ModuleType("h5py")
+    fake_h5py.File = _H5File
+    fake_sk = types.ModuleType("skimage")
+    fake_skr = types.ModuleType("skimage.restoration")
+    fake_skr.denoise_nl_means = skimage_denoise_nl_means(bridge)
+    fake_sk.restoration = fake_skr
+    saved = {k: sys.modules.get(k) for k in ("h5py", "skimage", "skimage.restoration")}
+    sys.modules.update({"h5py": fake_h5py, "skimage": fake_sk, "skimage.restoration": fake_skr})
+    sys.path.insert(0, REF)
+    scipy.io.loadmat = loadmat
+    snaps = {}
+    g = {"__name__": "__main__", "__file__": os.path.join(REF, "main_LRS_PnP.py")}
+
+    def hooked_print(*args, **kw):
+        if args and isinstance(args[0], str) and args[0].startswith("Outer-Loop Iteration"):
+            it = int(args[1])
+            sys.stderr.write(f"cfg0 iteration {it}\n")
+            if it in (1, 2):
+                snaps[it] = g["X"].clone().numpy()
+    g["print"] = hooked_print
+    try:
+        src = open(os.path.join(REF, "main_LRS_PnP.py")).read()
+        assert src.count("iteration_num = 2") == 1
+        src = src.replace("iteration_num = 2", f"iteration_num = {iters}")
+        torch.set_num_threads(8)
+        exec(compile(src, os.path.join(REF, "main_LRS_PnP.py"), "exec"), g)
+    finally:
+        scipy.io.loadmat = real_loadmat
+        sys.path.remove(REF)
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    mpsnr = np.array([float(v) for v in g["list_MPSNR"]], np.float64)
+    np.savez_compressed(os.path.join(HERE, "lrs_pnp_cfg0_50iter.npz"), mpsnr=mpsnr, X1=snaps.get(1), X2=snaps.get(2),
+                        X=g["X"].numpy(), L1=g["lambda_1"].numpy(), L2=g["lambda_2"].numpy(), iters=iters)
+    print("cfg0 MPSNR", mpsnr, file=sys.stderr)
+
+
 def main(argv):
     which = set(argv) or {"data", "nlm", "ista", "lrs"}
     bridge = Bridge()
@@ -263,6 +339,8 @@ def main(argv):
             gen_ista(bridge, data)
         if "lrs" in which:
             gen_lrs_pnp_2iter(bridge)
+        if "cfg0" in which:
+            gen_lrs_pnp_cfg0(bridge)
     finally:
         bridge.close()
 

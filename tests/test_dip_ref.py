@@ -120,10 +120,22 @@ def test_unet_sizes():
     assert not unet_size_ok(200, 200)
 
 
-def test_early_stop_restatement_logic():
-    es = dip_ref.EarlyStopRef(size=3, patience=2)
-    seq = [np.full(4, v, np.float32) for v in (0, 1, 0, 1, 1, 1, 1, 1)]
-    stops = [es.update(s, i) for i, s in enumerate(seq)]
-    # variance decreases once the ring is flat: 2/9 (i=2), 2/9 (i=3, not <), 2/9 -> wait 2 -> stop at 4? no:
-    assert es.vars[0] > 0
-    assert stops[-1] and es.stop_epoch is not None and es.stop_epoch >= 3
+def test_early_stop_restatement_vs_reference_golden(golden):
+    """oracle/dip_ref.EarlyStopRef (fp64 mean / variance) against the reference's own
+    get_DIP_out + EarlyStop + myMetric (tests/golden/gen_es_golden.py: float32 numpy) on three
+    recorded output trajectories: the same stop step (or none), every variance to 1e-5 relative
+    (float32 vs fp64 rounding of the same sums), the same best epoch."""
+    g = golden("es_golden.npz")
+    for k in range(3):
+        traj = g[f"traj{k}"]
+        es = dip_ref.EarlyStopRef(size=int(g["size"]), patience=int(g["patience"]))
+        ret = -1
+        for i in range(traj.shape[0]):
+            if es.update(traj[i], i):
+                ret = i
+                break
+        assert ret == int(g[f"ret{k}"]), k
+        n = len(g[f"var{k}"])
+        np.testing.assert_allclose(es.vars[:n], g[f"var{k}"], rtol=1e-5)
+        best_i = int(np.argmin(es.vars[:n]))
+        assert g[f"epoch{k}"][best_i] == int(g[f"best_epoch{k}"])

@@ -253,6 +253,34 @@ def test_early_stop_device_vs_reference_logic(L):
     np.testing.assert_allclose(st.best, min(ref.vars), rtol=1e-9)
 
 
+def test_early_stop_device_vs_reference_golden(L, golden):
+    """lrs_es_update_f32 against the reference's own get_DIP_out early stopping (EarlyStop +
+    myMetric, float32 numpy; tests/golden/gen_es_golden.py) on three recorded trajectories: the
+    device stops at the step where the reference returned (or never), its best variance matches
+    the reference's best_score to 1e-5 relative (fp64 vs float32 sums), and every variance it
+    computed (last_var) matches the reference's cur_var to 1e-5."""
+    from lrspnp.dip import EarlyStopper
+    g = golden("es_golden.npz")
+    for k in range(3):
+        traj = torch.from_numpy(g[f"traj{k}"]).cuda()
+        T, N = traj.shape[0], traj[0].numel()
+        es = EarlyStopper(N, int(g["size"]), int(g["patience"]))
+        ref_var = dict(zip(g[f"epoch{k}"].tolist(), g[f"var{k}"].tolist()))
+        stop_at = -1
+        for i in range(T):
+            assert L.lrs_es_update_f32(P(traj[i]), N, P(es.ring), P(es.state), None) == 0
+            st = es.read()
+            if i in ref_var:
+                assert abs(st.last_var - ref_var[i]) <= 1e-5 * ref_var[i], (k, i)
+            if st.stop and stop_at < 0:
+                stop_at = i
+                assert st.stop_epoch == i
+                break
+        assert stop_at == int(g[f"ret{k}"]), (k, stop_at)
+        assert abs(st.best - float(g[f"best{k}"])) <= 1e-5 * float(g[f"best{k}"])
+        assert st.best_epoch == int(g[f"best_epoch{k}"])
+
+
 # ---- whole network -----------------------------------------------------------------------------
 def _problem(gold_seed=1234, units=None):
     from gen_dip_golden import flat_params, problem

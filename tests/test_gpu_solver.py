@@ -113,6 +113,65 @@ def test_config2_shape_properties(gpu):
     assert np.isfinite([nx, n1, n2]).all() and nx > 0
 
 
+def _bench_problem(H, W, B, bb):
+    from lrspnp.data import load_fixture, mask_matrix, synthetic_cube, synthetic_dictionary, unfold
+    base = load_fixture("data_img5.npz")["lrs_mask"]
+    obs, clean, mask = synthetic_cube(H, W, B, seed=0, base_mask=base)
+    return unfold(obs), mask_matrix(mask, B), synthetic_dictionary(bb * bb, 256, 0), clean
+
+
+def test_config1_two_outer_iterations_vs_oracle_fixture(gpu, golden):
+    """BASELINE configs[1] end to end at full size (200x200x198, bb 8, 125,000 blocks, Nit 80):
+    two whole-cube outer iterations against the oracle's (tests/golden/gen_cube_oracle.py).
+    Tolerances: 1e-5 relative L2 on the row-strided X subsample (lambda_1 / lambda_2: see below), MPSNR and
+    every band's PSNR identical to 2 dp (north_star), the three state_convergence norms to 1e-4.
+    The oracle's MPSNR also falls from iteration 1 to 2 (32.136 -> 32.108), as the bench's does."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.metrics import psnr_bands
+    g = golden("cube200_oracle_2iter.npz")
+    Y, M, D, clean = _bench_problem(200, 200, 198, 8)
+    s = LrsPnP(Y, M, D, LrsPnPConfig(bb=8, sliding=8, Nit=80, variant="spec2"))
+    clean_d = torch.from_numpy(clean).cuda()
+    rows = torch.from_numpy(g["rows"]).cuda()
+    assert np.allclose(psnr_bands(s.X, clean_d).cpu().numpy(), g["psnr_input"], atol=5e-3)
+    for it in range(2):
+        s.step()
+        torch.cuda.synchronize()
+        Xr = g["X"][it]
+        got = s.X.index_select(0, rows).cpu().numpy()
+        assert rel(got, Xr) < 1e-5, (it, rel(got, Xr))
+        # the duals are mu (X - Phi) and mu (X - U): differences ~100x smaller than X, so their
+        # relative error is X's amplified by the cancellation (measured 1.2e-5 on lambda_2, the
+        # float32-LAPACK vs fp64-Gram SVT rounding).  Bound them at X's scale: ||d lambda|| <= 1e-5 mu ||X||
+        for name, mu, ref in (("L1", s.cfg.mu1, g["L1"][it]), ("L2", s.cfg.mu2, g["L2"][it])):
+            got = getattr(s, name).index_select(0, rows).cpu().numpy()
+            err = np.linalg.norm((got - ref).astype(np.float64))
+            assert err < 1e-5 * mu * np.linalg.norm(Xr.astype(np.float64)) and rel(got, ref) < 5e-5, (it, name, rel(got, ref))
+        p = psnr_bands(s.X, clean_d).cpu().numpy()
+        assert np.array_equal(np.round(p, 2), np.round(g["psnr"][it], 2)) or np.abs(p - g["psnr"][it]).max() < 5e-4
+        assert round(float(p.mean()), 2) == round(float(g["mpsnr"][it]), 2)
+        assert np.allclose(s.convergence(), g["norms"][it], rtol=1e-4)
+
+
+def test_config2_sparse_coding_vs_oracle_fixture(gpu, golden):
+    """BASELINE configs[2]'s sparse coding at full size (196x196x198, bb 36, 6,408 blocks, fro4,
+    Nit 100): the row-split ISTA kernel's Phi and coefficients of every 53rd block of the first
+    outer iteration against the oracle C ISTA at 1e-5 relative L2 (per block and overall)."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    g = golden("cube196_bb36_sc.npz")
+    Y, M, D, _ = _bench_problem(196, 196, 198, 36)
+    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_1lip(lowrank="svt"))
+    assert s.nb == 6408
+    phi, coefs = s.sparse_coding(want_coefs=True)
+    torch.cuda.synchronize()
+    sel = torch.from_numpy(g["blocks"]).cuda()
+    ph = phi.index_select(0, sel).cpu().numpy()[:, :1296]
+    co = coefs.index_select(0, sel).cpu().numpy()
+    assert rel(ph, g["phi"]) < 1e-5 and rel(co, g["coefs"]) < 1e-5
+    for k in range(sel.numel()):
+        assert rel(ph[k], g["phi"][k]) < 1e-5, k
+
+
 @pytest.mark.parametrize("world,cube", [(2, "96x64x40"), (3, "100x60x37")])
 def test_row_slab_sharding_matches_whole_cube(gpu, world, cube):
     """One cube in pixel-row slabs over `world` ranks (gloo, all on cuda:0): the

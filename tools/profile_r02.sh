@@ -21,4 +21,7 @@ for wl in ${WORKLOADS:-dip pnp}; do
   echo "== $wl sq"
   timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $out/${wl}_sq -o run --output-format csv -- python3 $B > $out/${wl}_sq.log 2>&1 || exit 1
 done
+# summarise on the box (the raw per-dispatch CSVs exceed what gpurun copies back), keep only the summary
+python tools/summarize_r02.py $out ${SUMDIR:-gpurun_out/r02sum} > $out/summary.log 2>&1 || { cat $out/summary.log; exit 1; }
+rm -rf $out/*_trace $out/*_fetch $out/*_write $out/*_sq
 echo profile-ok
