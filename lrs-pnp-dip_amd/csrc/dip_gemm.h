@@ -420,6 +420,161 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
         }
 }
 
+// ---- pointwise (1x1, stride 1, unpadded) conv product -----------------------------------------
+// C[M][N] (+)= A[M][Kp] B[K][N] (+ bias[M]) for M <= 256 output channels over N pixels: the
+// forward (A = the k_wprep forward planes WF, B = x) and the data gradient (A = WD = W^T planes,
+// B = dL/dz) of the reference's 1x1 convs (my_Lipschitz_Unet.py:96-103, skip.py's 1x1 skips).
+// One workgroup per 64 pixels: their B columns (all K) are read from HBM once and split into the
+// three bf16 planes in LDS ([plane][pixel][k], row stride ldsrow bytes = 16 mod 256 so the 16
+// pixel rows of a fragment read sit in distinct bank groups); the pre-split A fragments stream
+// from L2 (one k-step prefetched), so every C element of the 64 pixels is produced by this one
+// workgroup: no split-K, no tile quantisation on M.  Wave w owns rows 16 w + 64 j (j < MT).
+struct PwArgs {
+    const __bf16 *A;
+    int64_t pstride;   // plane stride of A (elements)
+    int lda;           // A row length (Kp, multiple of 16; columns >= the valid K are zero)
+    const float *B;
+    int K;             // valid B rows
+    int64_t N;
+    float *C;
+    const float *bias;
+    int M, Kp32, ldsrow, accum;
+    int dbg;   // diagnostics only (LRS_PW_DBG): 1 no C stores, 2 no A loads, 4 no B loads
+};
+
+inline int pw_ldsrow(int Kp32) {   // bytes; Kp32 * 2 rounded up to 16 mod 256
+    int b = Kp32 * 2;
+    return b + (((16 - b) % 256) + 256) % 256;
+}
+
+template <int MT>
+__global__ __launch_bounds__(256) void k_pw(PwArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char pw_smem[];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, jl = lane & 15, gk = lane >> 4;
+    const int64_t n0 = (int64_t)blockIdx.x * 64;
+    const int64_t plane = (int64_t)64 * a.ldsrow;
+    {   // stage: thread (n = t & 63) splits k chunks (t >> 6) + 4 i of 8 values each.  Buffer
+        // loads, branch-free: k (wave-uniform) goes in the scalar offset, so rows k >= K fall past
+        // the buffer's K * N floats and read 0; a pixel n >= N reads at kOob.
+        const int n = t & 63;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(a.B, (int)(a.K * a.N * 4));
+        const int voff = n0 + n < a.N ? (int)((n0 + n) * 4) : kOob;
+        const int nck = a.Kp32 / 8, c0 = __builtin_amdgcn_readfirstlane(t >> 6);
+        float v[8][8];   // all of the thread's chunks (<= 8 for K <= 256) in flight together
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = c0 + 4 * i;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t so = (int64_t)(8 * c + u) * a.N * 4;
+                v[i][u] = (c < nck && !(a.dbg & 4)) ? s3_bload(rs, voff, so < kOob ? (int)so : kOob) : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = c0 + 4 * i;
+            if (c >= nck) break;
+            s3bf8 p0, p1, p2;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const S3Split q = s3_split(v[i][u]);
+                p0[u] = q.b0;
+                p1[u] = q.b1;
+                p2[u] = q.b2;
+            }
+            char *dst = pw_smem + (int64_t)n * a.ldsrow + 16 * c;
+            *reinterpret_cast<s3bf8 *>(dst) = p0;
+            *reinterpret_cast<s3bf8 *>(dst + plane) = p1;
+            *reinterpret_cast<s3bf8 *>(dst + 2 * plane) = p2;
+        }
+    }
+    s3f4 acc[MT][4];
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[j][b] = s3f4{0.f, 0.f, 0.f, 0.f};
+    const int ksteps = a.Kp32 / 32;
+    s3bf8 fa[MT][3], fn[MT][3];
+    // A fragments: 16-B buffer loads (L2-resident planes), rows >= M and k >= lda at kOob (zeros)
+    const __amdgpu_buffer_rsrc_t ra = s3_rsrc(a.A, (int)(3 * a.pstride * 2));
+    auto loadA = [&](int ks, s3bf8 (&f)[MT][3]) {
+        const int k = ks * 32 + 8 * gk;
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            const int row = 16 * wv + 64 * j + jl;
+            const int vo = (row < a.M && k < a.lda && !(a.dbg & 2)) ? 2 * (row * a.lda + k) : kOob;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                f[j][p] = __builtin_bit_cast(s3bf8, __builtin_amdgcn_raw_buffer_load_b128(ra, vo, (int)(2 * p * a.pstride), 0));
+        }
+    };
+    loadA(0, fa);
+    __syncthreads();
+    for (int ks = 0; ks < ksteps; ++ks) {
+        if (ks + 1 < ksteps) loadA(ks + 1, fn);
+        s3bf8 fb[4][3];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const char *s0 = pw_smem + (int64_t)(16 * b + jl) * a.ldsrow + 16 * (4 * ks + gk);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) fb[b][p] = *reinterpret_cast<const s3bf8 *>(s0 + p * plane);
+        }
+#pragma unroll
+        for (int j = 0; j < MT; ++j)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) acc[j][b] = s3_mfma6(fa[j], fb[b], acc[j][b]);
+        if (ks + 1 < ksteps) {
+#pragma unroll
+            for (int j = 0; j < MT; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) fa[j][p] = fn[j][p];
+        }
+    }
+    // epilogue through LDS (the B image is dead after this barrier): wave w writes its 16 x 64 tile
+    // of each row block as [row][pixel] and reads it back as float4 rows, so every 16 lanes store
+    // one full 256-B pixel run of a channel row (the MFMA layout gives a lane 4 rows of 1 pixel)
+    __syncthreads();
+    float *E = reinterpret_cast<float *>(pw_smem) + wv * 16 * 68;
+    const bool vec = (a.N & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.C) & 15) == 0);
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) E[(4 * gk + r) * 68 + 16 * b + jl] = acc[j][b][r];
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done (wave-local tile)
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int idx = lane + 64 * i, rr = idx >> 4, q = 4 * (idx & 15);
+            const int m = 16 * wv + 64 * j + rr;
+            const int64_t n = n0 + q;
+            if (m >= a.M || (a.dbg & 1)) continue;
+            float4 v = *reinterpret_cast<const float4 *>(E + rr * 68 + q);
+            const float bs = a.bias ? a.bias[m] : 0.0f;
+            float *c = a.C + (int64_t)m * a.N + n;
+            if (vec && n + 3 < a.N) {
+                if (a.bias) { v.x = v.x + bs; v.y = v.y + bs; v.z = v.z + bs; v.w = v.w + bs; }
+                if (a.accum) {
+                    const float4 o = *reinterpret_cast<const float4 *>(c);
+                    v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
+                }
+                *reinterpret_cast<float4 *>(c) = v;
+            } else {
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+                for (int u = 0; u < 4; ++u) {
+                    if (n + u >= a.N) break;
+                    float x = vv[u];
+                    if (a.bias) x = x + bs;
+                    if (a.accum) x = c[u] + x;
+                    c[u] = x;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // Per conv weight W [Cout][Cin][kk] (fp32): the three bf16 planes of the forward operand
 // WF[p][co][kyx * Cp + c] and of the data-gradient operand WD[p][ci][kyx * Cop + co]
 // (Cp, Cop: Cin, Cout rounded up to 16; padding zero).  WD nullable.

@@ -895,54 +895,114 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd1(BnBwdArgs a) {
 // Gram on the smaller side (m = min(rows, cols) <= 128) in fp64, exact products.
 // ------------------------------------------------------------------------------------------
 constexpr int kSnMaxDim = 128;
-constexpr int kSnSplit = 8;   // inner-dimension split of the Gram (partials summed in k_sn_sigma)
+constexpr int kSnSplit = 16;  // inner-dimension split of the Gram (partials reduced by k_sn_gram_reduce)
+constexpr int kSnPairs = 36;  // upper 16 x 16 tile pairs of a 128 x 128 Gram
+// Gram workspace per conv (doubles): the reduced symmetric Gram [128][128], then the split
+// partials [kSnSplit][kSnPairs][16 * 16]
+constexpr int64_t kSnGramDoubles = (int64_t)kSnMaxDim * kSnMaxDim + (int64_t)kSnSplit * kSnPairs * 256;
 
-// grid (tiles^2, kSnSplit, n): partial z of the Gram tile (ti, tj) over its inner range
-__global__ __launch_bounds__(256) void k_sn_gram(const SnConv *convs, double *gram) {
-    const SnConv cv = convs[blockIdx.z];
-    const bool rowside = cv.rows <= cv.cols;    // G = W W^T (rows) or W^T W (cols)
+typedef double sn_d4 __attribute__((ext_vector_type(4)));
+
+struct SnPairs {
+    int a[kSnPairs], b[kSnPairs];
+};
+__host__ __device__ constexpr SnPairs sn_pairs() {
+    SnPairs t{};
+    int k = 0;
+    for (int a = 0; a < 8; ++a)
+        for (int b = a; b < 8; ++b) {
+            t.a[k] = a;
+            t.b[k] = b;
+            ++k;
+        }
+    return t;
+}
+
+template <int W, int... U>
+__device__ __forceinline__ void sn_mfmas(const double (&f)[8], sn_d4 (&acc)[9], std::integer_sequence<int, U...>) {
+    constexpr SnPairs P = sn_pairs();
+    ((acc[U] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[P.a[W + 4 * U]], f[P.b[W + 4 * U]], acc[U], 0, 0, 0)), ...);
+}
+
+// grid (kSnSplit, n), 256 threads: partial z of the 36 upper 16 x 16 tile pairs of the fp64 Gram
+// (G = W W^T on the smaller side, m <= 128) over the z-th inner range, on v_mfma_f64_16x16x4
+// (exact products of float32 values, fp64 sums).  W is staged 32 inner values at a time in LDS as
+// [row][k] floats (row stride 36: the 16 rows x 4 k of a fragment read hit 64 distinct banks); a
+// lane's A and B fragments are W[16 c + (l & 15)][k + (l >> 4)] (the same form for both
+// operands), wave w owns the pairs w, w + 4, ..., w + 32.
+template <int WV>
+__device__ __forceinline__ void sn_gram_body(const SnConv &cv, float (*Ws)[36], double *out) {
+    const bool rowside = cv.rows <= cv.cols;
     const int m = rowside ? cv.rows : cv.cols;
     const int inner = rowside ? cv.cols : cv.rows;
-    const int tiles = (m + 31) / 32;
-    if ((int)blockIdx.x >= tiles * tiles) return;
-    const int ti = blockIdx.x / tiles, tj = blockIdx.x % tiles;
     const int per = (int)round_up((inner + kSnSplit - 1) / kSnSplit, 32);
-    const int kb = blockIdx.y * per, ke = min(inner, kb + per);
-    __shared__ float Si[32][33], Sj[32][33];
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 8 rows of 32
-    double acc[4] = {0, 0, 0, 0};
-    double *G = gram + ((int64_t)blockIdx.z * kSnSplit + blockIdx.y) * kSnMaxDim * kSnMaxDim;
+    const int kb = blockIdx.x * per, ke = min(inner, kb + per);
+    const int t = threadIdx.x, lane = t & 63, g = lane >> 4, jl = lane & 15;
+    sn_d4 acc[9];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) acc[u] = sn_d4{0.0, 0.0, 0.0, 0.0};
     for (int k0 = kb; k0 < ke; k0 += 32) {
-        for (int e = threadIdx.x; e < 32 * 32; e += 256) {
-            const int r = e >> 5, kk = e & 31;
-            const int ii = ti * 32 + r, jj = tj * 32 + r, k = k0 + kk;
-            float vi = 0.f, vj = 0.f;
-            if (k < ke) {
-                if (rowside) {
-                    if (ii < m) vi = cv.W[(int64_t)ii * cv.cols + k];
-                    if (jj < m) vj = cv.W[(int64_t)jj * cv.cols + k];
-                } else {
-                    if (ii < m) vi = cv.W[(int64_t)k * cv.cols + ii];
-                    if (jj < m) vj = cv.W[(int64_t)k * cv.cols + jj];
-                }
-            }
-            Si[r][kk] = vi;
-            Sj[r][kk] = vj;
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = t + 256 * u;
+            const int r = rowside ? (e >> 5) : (e & 127), kk = rowside ? (e & 31) : (e >> 7);
+            const int k = k0 + kk;
+            v[u] = (r < m && k < ke) ? (rowside ? cv.W[(int64_t)r * cv.cols + k] : cv.W[(int64_t)k * cv.cols + r]) : 0.f;
         }
         __syncthreads();
-#pragma unroll 4
-        for (int kk = 0; kk < 32; ++kk) {
-            const double b = (double)Sj[tx][kk];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = __fma_rn((double)Si[ty + 8 * q][kk], b, acc[q]);
+        for (int u = 0; u < 16; ++u) {
+            const int e = t + 256 * u;
+            const int r = rowside ? (e >> 5) : (e & 127), kk = rowside ? (e & 31) : (e >> 7);
+            Ws[r][kk] = v[u];
         }
         __syncthreads();
-    }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int i = ti * 32 + ty + 8 * q, j = tj * 32 + tx;
-        if (i < m && j < m) G[i * kSnMaxDim + j] = acc[q];
+        for (int kq = 0; kq < 32; kq += 4) {
+            double f[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) f[c] = (double)Ws[16 * c + jl][kq + g];
+            sn_mfmas<WV>(f, acc, std::make_integer_sequence<int, 9>{});
+        }
     }
+    // C/D layout of the f64 MFMA: column l & 15, row (l >> 4) + 4 r
+#pragma unroll
+    for (int u = 0; u < 9; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(int64_t)(WV + 4 * u) * 256 + (g + 4 * r) * 16 + jl] = acc[u][r];
+}
+
+__global__ __launch_bounds__(256) void k_sn_gram(const SnConv *convs, double *gram) {
+    __shared__ float Ws[128][36];
+    const SnConv cv = convs[blockIdx.y];
+    double *out = gram + (int64_t)blockIdx.y * kSnGramDoubles + (int64_t)kSnMaxDim * kSnMaxDim +
+                  (int64_t)blockIdx.x * kSnPairs * 256;
+    switch (threadIdx.x >> 6) {
+    case 0: sn_gram_body<0>(cv, Ws, out); break;
+    case 1: sn_gram_body<1>(cv, Ws, out); break;
+    case 2: sn_gram_body<2>(cv, Ws, out); break;
+    default: sn_gram_body<3>(cv, Ws, out); break;
+    }
+}
+
+// grid (kSnPairs, n): tile pair p, element q of its 16 x 16 block (coalesced partial reads): the
+// sum over z (in order) of the partials, stored at G[i][j] and mirrored to G[j][i]; G is m x m
+// inside the 128 x 128 buffer (the staged rows >= m were zero, so entries outside are 0).
+__global__ __launch_bounds__(256) void k_sn_gram_reduce(const SnConv *convs, double *gram) {
+    constexpr SnPairs PT = sn_pairs();
+    const int p = blockIdx.x, q = threadIdx.x;
+    const int i = 16 * PT.a[p] + (q >> 4), j = 16 * PT.b[p] + (q & 15);
+    double *G = gram + (int64_t)blockIdx.y * kSnGramDoubles;
+    const double *part = G + (int64_t)kSnMaxDim * kSnMaxDim + (int64_t)p * 256 + q;
+    double pv[kSnSplit];
+#pragma unroll
+    for (int z = 0; z < kSnSplit; ++z) pv[z] = part[(int64_t)z * kSnPairs * 256];
+    double v = 0.0;
+#pragma unroll
+    for (int z = 0; z < kSnSplit; ++z) v += pv[z];
+    G[i * kSnMaxDim + j] = v;
+    if (PT.a[p] != PT.b[p]) G[j * kSnMaxDim + i] = v;
 }
 
 // number of eigenvalues of the symmetric tridiagonal (diag al, squared off-diagonal be2) above x:
@@ -951,18 +1011,19 @@ __global__ __launch_bounds__(256) void k_sn_gram(const SnConv *convs, double *gr
 // sign).  Four terms per block: their eight LDS reads are issued together, off the serial chain.
 // (Measured: holding al / be2 in registers and broadcasting with readlane is slower.)
 __device__ __forceinline__ void sturm_term(double a, double b2, double x, double &p, double &pm, int &changes) {
-    const double pn = __fma_rn(a - x, p, -b2 * pm);
-    // sign change between p_{i-1} and p_i (a zero takes the sign opposite to its predecessor)
-    const bool neg_prev = (p < 0.0) || (p == 0.0 && pm > 0.0);
-    const bool neg_cur = (pn < 0.0) || (pn == 0.0 && !neg_prev);
-    changes += neg_prev != neg_cur;
+    double pn = __fma_rn(a - x, p, -b2 * pm);
+    // a zero takes the sign opposite to its predecessor: perturb it to -p * 2^-600 (the usual
+    // Sturm-sequence convention; the next term is then -b2 p (1 + O(2^-600)))
+    pn = pn != 0.0 ? pn : -p * 0x1p-600;
+    changes += (int)((unsigned long long)(__double_as_longlong(pn) ^ __double_as_longlong(p)) >> 63);
     pm = p;
     p = pn;
 }
 
 __device__ int sturm_gt(const double *al, const double *be2, int k, double x) {
     double pm = 1.0, p = al[0] - x;
-    int changes = (p < 0.0) || (p == 0.0);   // p_0 = 1 > 0
+    p = p != 0.0 ? p : -0x1p-600;              // p_0 = 1 > 0: a zero p_1 counts as negative
+    int changes = p < 0.0;
     int i = 1;
     for (; i + 4 <= k; i += 4) {
         const double a0 = al[i], a1 = al[i + 1], a2 = al[i + 2], a3 = al[i + 3];
@@ -1029,18 +1090,24 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     if (prof && threadIdx.x == 0) prof[blockIdx.x * 8 + 0] = wall_clock64();
     const SnConv cv = convs[blockIdx.x];
     const int m = cv.rows <= cv.cols ? cv.rows : cv.cols;
-    const double *G = gram + (int64_t)blockIdx.x * kSnSplit * kSnMaxDim * kSnMaxDim;
+    const double *G = gram + (int64_t)blockIdx.x * kSnGramDoubles;
     extern __shared__ double Gs[];                // [kSnMaxDim][kSnMaxDim + 1] (dynamic, 129 KB)
-    __shared__ double q[kSnMaxDim], al[kSnMaxDim], be[kSnMaxDim], be2[kSnMaxDim], lohi[2];
+    __shared__ __attribute__((aligned(16))) double q[kSnMaxDim];
+    __shared__ double al[kSnMaxDim], be[kSnMaxDim], be2[kSnMaxDim], lohi[2];
     __shared__ int best_s;
     const int t = threadIdx.x, row = t >> 1, half = t & 1;
     // sum the split-K partials with coalesced loads into LDS, then each thread takes half a row
-    for (int e = t; e < kSnMaxDim * kSnMaxDim; e += blockDim.x) {
-        const int r = e / kSnMaxDim, c = e % kSnMaxDim;
-        double v = 0.0;
-        if (r < m && c < m)
-            for (int z = 0; z < kSnSplit; ++z) v += G[(int64_t)z * kSnMaxDim * kSnMaxDim + e];
-        Gs[r * (kSnMaxDim + 1) + c] = v;
+    // the reduced Gram (k_sn_gram_reduce): 16-B loads, all in flight
+    {
+        double2 pv[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) pv[u] = *reinterpret_cast<const double2 *>(G + 2 * (t + 256 * u));
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const int e = 2 * (t + 256 * u), r = e / kSnMaxDim, c = e % kSnMaxDim;
+            Gs[r * (kSnMaxDim + 1) + c] = pv[u].x;
+            Gs[r * (kSnMaxDim + 1) + c + 1] = pv[u].y;
+        }
     }
     __syncthreads();
     double g[64];
@@ -1062,9 +1129,20 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     int k = 0;
     bool converged = false;
     for (; k < m; ++k) {
+        // all 32 b128 reads of this thread's half of q are issued before the first FMA (left to
+        // itself the compiler waited on each read: ~2.5 us per step instead of ~0.5)
+        double qv[64];
+        const double2 *q2 = reinterpret_cast<const double2 *>(q + half * 64);
+#pragma unroll
+        for (int c = 0; c < 32; ++c) {
+            const double2 v = q2[c];
+            qv[2 * c] = v.x;
+            qv[2 * c + 1] = v.y;
+        }
+        __builtin_amdgcn_sched_barrier(0);
         double acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};    // 8 independent FMA chains
 #pragma unroll
-        for (int c = 0; c < 64; ++c) acc8[c & 7] = __fma_rn(g[c], q[half * 64 + c], acc8[c & 7]);
+        for (int c = 0; c < 64; ++c) acc8[c & 7] = __fma_rn(g[c], qv[c], acc8[c & 7]);
         double u = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
         u += __shfl_xor(u, 1, 64);
         const double w_rr = wave_sum_d(half == 0 ? rr * rr : 0.0);
@@ -1101,9 +1179,9 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     }
     __syncthreads();
     if (prof && t == 0) { prof[blockIdx.x * 8 + 2] = wall_clock64(); prof[blockIdx.x * 8 + 4] = k; }
-    // converged at a check: T_k is the matrix that check bracketed (4 rounds); 2 more rounds
-    // give the same 1e-15 width as 8 rounds from the Gershgorin interval
-    const double lmax = m > 0 ? tridiag_max_eig(al, be, be2, k, converged ? 2 : 8, lohi, &best_s, converged) : 0.0;
+    // converged at a check: that check's bracket (4 rounds from Gershgorin, width <= ~1e-9 lmax,
+    // far below the float32 rounding of sigma) is the result; else 8 rounds from Gershgorin
+    const double lmax = m <= 0 ? 0.0 : converged ? 0.5 * (lohi[0] + lohi[1]) : tridiag_max_eig(al, be, be2, k, 8, lohi, &best_s);
     if (prof && t == 0) prof[blockIdx.x * 8 + 3] = wall_clock64();
     if (t == 0) {
         const float s32 = (float)sqrt(fmax(lmax, 0.0));

@@ -218,12 +218,47 @@ void wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, 
                        wf, wd);
 }
 
+// Pointwise conv product on k_pw (A: pre-split planes [3][M][lda], B: [K][N] fp32).
+int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, int K, int64_t N, float *C,
+              const float *bias, int accum, hipStream_t st) {
+    if (M <= 0 || N <= 0) return LRS_OK;
+    if (M > 256 || lda < K || lda % 16) return LRS_E_UNSUPPORTED;
+    const int Kp32 = (int)round_up(lda, 32), ldsrow = pw_ldsrow(Kp32);
+    const int lds = 3 * 64 * ldsrow;
+    static bool attr_set = false;
+    if (!attr_set) {   // up to K = 256: 3 x 64 x 528 B
+        const int mx = 3 * 64 * pw_ldsrow(256);
+        hipError_t e = hipFuncSetAttribute((const void *)k_pw<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<4>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        if (e != hipSuccess) return (int)e;
+        attr_set = true;
+    }
+    if (Kp32 > 256 || (int64_t)K * N * 4 >= kOob || 3 * pstride * 2 >= kOob) return LRS_E_UNSUPPORTED;
+    static const int dbg = getenv("LRS_PW_DBG") ? atoi(getenv("LRS_PW_DBG")) : 0;
+    const PwArgs a{A, pstride, lda, B, K, N, C, bias, M, Kp32, ldsrow, accum, dbg};
+    const dim3 grid((unsigned)((N + 63) / 64));
+    switch ((M + 63) / 64) {
+    case 1: hipLaunchKernelGGL(k_pw<1>, grid, dim3(256), lds, st, a); break;
+    case 2: hipLaunchKernelGGL(k_pw<2>, grid, dim3(256), lds, st, a); break;
+    case 3: hipLaunchKernelGGL(k_pw<3>, grid, dim3(256), lds, st, a); break;
+    default: hipLaunchKernelGGL(k_pw<4>, grid, dim3(256), lds, st, a); break;
+    }
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+inline bool pw_ok(const ConvGeom &g, int Cout) { return plain_unit(g) && Cout <= 256 && r16(g.Cin) <= 256 && r16(Cout) <= 256; }
+
 // y = conv(x) + bias.  Explicit (col != NULL): im2col + GEMM.  Implicit (col == NULL, wpre =
 // the weight planes from wprep): tap-major implicit GEMM.
 int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bias, int Cout, float *col, float *y,
              float *part, int64_t part_cap, hipStream_t st, const __bf16 *wpre = nullptr) {
     const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
     const float *B = x;
+    if (plain_unit(g) && wpre)      // 1x1: pointwise kernel on the pre-split weights
+        return pw_launch(wpre, (int64_t)Cout * r16(g.Cin), r16(g.Cin), Cout, x, g.Cin, P, y, bias, 0, st);
     if (!plain_unit(g) && !col) {   // implicit im2col
         if (!conv_implicit_ok(g, Cout) || !wpre) return LRS_E_UNSUPPORTED;
         const int kk = g.k * g.k, Cp = r16(g.Cin);
@@ -259,6 +294,9 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
     }
     if (rc || !gx) return rc;
+    if (plain_unit(g) && wpre)      // 1x1 data gradient: W^T planes (wprep's WD)
+        return pw_launch(wpre + wprep_fwd_elems(g, Cout), (int64_t)g.Cin * r16(Cout), r16(Cout), g.Cin, gz, Cout, P,
+                         gx, nullptr, accum_gx, st);
     if (plain_unit(g)) return gemm(1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st, accum_gx);
     if (!dcol) return LRS_E_WORKSPACE;
     const int Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad);
@@ -337,8 +375,8 @@ int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, 
 
 int sn_launch(const SnConv *table_dev, int n, int64_t max_elems, double *gram, float *sigma, float *scale,
               float ln_lambda, bool apply, hipStream_t st, long long *prof = nullptr) {
-    const int tiles = (kSnMaxDim + 31) / 32;
-    hipLaunchKernelGGL(k_sn_gram, dim3(tiles * tiles, kSnSplit, n), dim3(256), 0, st, table_dev, gram);
+    hipLaunchKernelGGL(k_sn_gram, dim3(kSnSplit, n), dim3(256), 0, st, table_dev, gram);
+    hipLaunchKernelGGL(k_sn_gram_reduce, dim3(kSnPairs, n), dim3(256), 0, st, table_dev, gram);
     const size_t lds = sizeof(double) * kSnMaxDim * (kSnMaxDim + 1);
     hipError_t e = hipFuncSetAttribute((const void *)k_sn_sigma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
@@ -444,7 +482,7 @@ inline ConvWs conv_ws(const ConvGeom &g, int Cout) {
     ConvWs w;
     w.dcol = plain_unit(g) ? 0 : (int64_t)g.Cin * g.k * g.k * g.Ho * g.Wo;
     w.part = conv_part_floats(g, Cout);
-    w.wpre_floats = plain_unit(g) ? 0 : (wprep_elems(g, Cout) + 7) / 2;
+    w.wpre_floats = (plain_unit(g) && !pw_ok(g, Cout)) ? 0 : (wprep_elems(g, Cout) + 7) / 2;
     return w;
 }
 
@@ -462,8 +500,9 @@ extern "C" int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const f
     int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
     if (rc) return rc;
     if (!x || !w || !y || Cout <= 0) return LRS_E_INVALID;
-    const bool implicit = !col && !plain_unit(g);
-    if (implicit && !conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
+    // col == NULL: implicit GEMM, or for a 1x1 conv the pointwise kernel on pre-split weights
+    const bool implicit = !col && (!plain_unit(g) || pw_ok(g, Cout));
+    if (implicit && !plain_unit(g) && !conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
     const ConvWs cw = conv_ws(g, Cout);
     const int64_t need = implicit ? cw.dcol + cw.part + cw.wpre_floats : cw.part;
     if (need > 0 && (!ws || ws_bytes < (size_t)need * sizeof(float))) return LRS_E_WORKSPACE;
@@ -542,7 +581,7 @@ extern "C" int lrs_bn_act_bwd_f32(const float *gy, const float *y, const float *
 
 extern "C" size_t lrs_sigma_max_workspace(int n) {
     if (n <= 0) return 0;
-    return (size_t)n * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double) + (size_t)n * sizeof(SnConv) + 256;
+    return (size_t)n * kSnGramDoubles * sizeof(double) + (size_t)n * sizeof(SnConv) + 256;
 }
 
 extern "C" int lrs_sigma_max_f32(const float *const *W, float *const *Wn, const int *rows, const int *cols, int n,
@@ -561,7 +600,7 @@ extern "C" int lrs_sigma_max_f32(const float *const *W, float *const *Wn, const 
         if (e > maxe) maxe = e;
     }
     double *gram = (double *)ws;
-    SnConv *tdev = (SnConv *)((char *)ws + (size_t)n * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double));
+    SnConv *tdev = (SnConv *)((char *)ws + (size_t)n * kSnGramDoubles * sizeof(double));
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemcpyAsync(tdev, tab.data(), sizeof(SnConv) * n, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return (int)e;
@@ -579,7 +618,7 @@ extern "C" int lrs_diag_sigma_phases(const float *const *W, const int *rows, con
     std::vector<SnConv> tab(n);
     for (int i = 0; i < n; ++i) tab[i] = SnConv{W[i], nullptr, rows[i], cols[i]};
     double *gram = (double *)ws;
-    SnConv *tdev = (SnConv *)((char *)ws + (size_t)n * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double));
+    SnConv *tdev = (SnConv *)((char *)ws + (size_t)n * kSnGramDoubles * sizeof(double));
     float *sig = (float *)((char *)ws + lrs_sigma_max_workspace(n));
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemcpyAsync(tdev, tab.data(), sizeof(SnConv) * n, hipMemcpyHostToDevice, st);
@@ -899,6 +938,10 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                 N.wn_off = ofs; ofs += align64(N.C * N.Kc);
                 if (N.C * N.Kc > net->max_w) net->max_w = N.C * N.Kc;
             }
+            if (plain_unit(N.g) && net->implicit && pw_ok(N.g, N.C) && N.P >= implicit_min_pixels()) {
+                N.wpre_off = ofs;   // 1x1 on k_pw: its pre-split weight planes
+                ofs += align64((wprep_elems(N.g, N.C) + 1) / 2);
+            }
             if (!plain_unit(N.g)) {
                 if (!(net->implicit && conv_implicit_ok(N.g, N.C) && N.P >= implicit_min_pixels())) {
                     N.col_off = ofs;
@@ -969,7 +1012,7 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     net->scale_off = ofs; ofs += align64(n_sn > 0 ? n_sn : 1);
     size_t bytes = (size_t)ofs * sizeof(float);
     net->gram_off_bytes = (int64_t)bytes;
-    bytes += (size_t)n_sn * kSnSplit * kSnMaxDim * kSnMaxDim * sizeof(double);
+    bytes += (size_t)n_sn * kSnGramDoubles * sizeof(double);
     net->bnpart_off_bytes = (int64_t)bytes;
     bytes += (size_t)round_up((max_bnpart > 0 ? max_bnpart : 1) * (int64_t)sizeof(double), 256);
     net->table_off_bytes = (int64_t)bytes;

@@ -56,6 +56,9 @@ CONV_CASES = [
     (5, 9, 5, 7, 3, 1, 1, 1, 1),
     (128, 128, 196, 196, 3, 1, 1, 1, 0),    # 196x196 layer: 128x128 GEMM tiles (split-bf16 path)
     (64, 96, 100, 90, 3, 2, 1, 0, 0),       # 128-tiles with ragged M, N and K
+    (128, 198, 196, 196, 1, 1, 0, 1, 0),    # 196x196 last 1x1 (k_pw with col == NULL: 4 row blocks)
+    (198, 128, 40, 41, 1, 1, 0, 1, 0),      # k_pw: K = 198 (planes padded to 208), N % 64 != 0
+    (37, 250, 9, 13, 1, 1, 0, 1, 0),        # k_pw: ragged K, M = 250
 ]
 
 

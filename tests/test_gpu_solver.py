@@ -57,6 +57,34 @@ def test_two_outer_iterations_vs_reference(gpu, golden):
     assert round(p2, 2) == round(float(g["mpsnr"][1]), 2)
 
 
+def test_config0_fifty_outer_iterations_vs_reference(gpu, golden):
+    """BASELINE configs[0] as written: main_LRS_PnP.py's 50 outer iterations on
+    low_rank_sparsity_noisy.mat + fourth_mask.mat (the reference itself, run by
+    tests/golden/gen_golden.py cfg0).  X after iterations 1, 2 and 50 and lambda_1 / lambda_2 after
+    50 to 1e-5 relative L2, the MPSNR of every one of the 50 iterations identical to 2 dp."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.data import synthetic_dictionary, unfold, mask_matrix
+    from lrspnp.metrics import mpsnr
+    d = golden("data_img5.npz")
+    g = golden("lrs_pnp_cfg0_50iter.npz")
+    s = LrsPnP(unfold(d["noisy"][0]), mask_matrix(d["fourth_mask"], 128), synthetic_dictionary(1296, 256, 0),
+               LrsPnPConfig(bb=36, sliding=36, Nit=80, variant="spec2"))
+    clean = torch.from_numpy(d["clean"][0]).cuda()
+    mps = []
+    for it in range(50):
+        s.step()
+        mps.append(mpsnr(s.X, clean))
+        if it in (0, 1):
+            torch.cuda.synchronize()
+            ref = g["X1"] if it == 0 else g["X2"]
+            assert rel(s.X.cpu().numpy(), ref) < 1e-5, it
+    torch.cuda.synchronize()
+    assert rel(s.X.cpu().numpy(), g["X"]) < 1e-5
+    assert rel(s.L1.cpu().numpy(), g["L1"]) < 1e-5
+    assert rel(s.L2.cpu().numpy(), g["L2"]) < 1e-5
+    assert np.array_equal(np.round(mps, 2), np.round(g["mpsnr"], 2)), (mps, g["mpsnr"])
+
+
 def test_dip_variant_sparse_coding_matches_oracle(gpu, golden):
     """ISTA rule of the DIP mains (alpha = 4||H||_F^2, h = T, Nit = 100) on the native data."""
     from lrspnp import LrsPnP, LrsPnPConfig
@@ -172,14 +200,17 @@ def test_config2_sparse_coding_vs_oracle_fixture(gpu, golden):
         assert rel(ph[k], g["phi"][k]) < 1e-5, k
 
 
-@pytest.mark.parametrize("world,cube", [(2, "96x64x40"), (3, "100x60x37")])
-def test_row_slab_sharding_matches_whole_cube(gpu, world, cube):
+@pytest.mark.parametrize("world,cube,bb", [(2, "96x64x40", 8), (3, "100x60x37", 8), (3, "100x61x37", 8),
+                                           (2, "38x38x40", 36)])
+def test_row_slab_sharding_matches_whole_cube(gpu, world, cube, bb):
     """One cube in pixel-row slabs over `world` ranks (gloo, all on cuda:0): the
     sharded solver (slab-local sparse coding / col2im / updates, all-reduced fp64 SVT Gram)
     reproduces the whole-cube solver. Tolerance 1e-6 relative L2 after 3 outer iterations: the
     slabs sum the fp64 Gram in another order, everything else is the same per-block arithmetic.
-    100x60 with bb 8 leaves a 4-row tail (the appended block row) on the last rank, 37 bands an
-    odd Gram size."""
+    100x60 (P = 6000, a multiple of bb = 8) splits into ragged slabs of whole block rows and 37 bands
+    give an odd Gram size; 100x61 (P = 6100, P % 8 = 4) and 38x38x40 with bb 36 (P = 1444, P % 36 = 4:
+    the 200x200 / 196x196 configs' case) put the appended block row at P - bb, overlapping the
+    previous block row, on the last rank."""
     import json
     import os
     import socket
@@ -192,7 +223,7 @@ def test_row_slab_sharding_matches_whole_cube(gpu, world, cube):
     so.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(repo, "tools", "shard_check.py"),
-           "--backend", "gloo", "--cube", cube, "--steps", "3"]
+           "--backend", "gloo", "--cube", cube, "--steps", "3", "--bb", str(bb)]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=repo)
     assert p.returncode == 0, p.stderr[-3000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]

@@ -108,3 +108,22 @@ def test_nlm_matlab_closed_form_vs_literal():
         literal = O.nlm_matlab_literal(g.reshape(-1, 1).astype(np.float64), 3, 3, h).reshape(-1)
         np.testing.assert_allclose(closed, literal.astype(np.float32), rtol=2e-7, atol=1e-9)
         assert np.abs(closed - g).max() > 0      # the filter is not the identity at these h
+
+
+def test_config0_oracle_vs_reference_first_iterations(golden):
+    """BASELINE configs[0] as written (tests/golden/gen_golden.py cfg0: the reference's
+    main_LRS_PnP.py run for 50 outer iterations on low_rank_sparsity_noisy.mat + fourth_mask.mat):
+    the oracle's first two iterates (X to 1e-6 relative) and MPSNR of three iterations to 4 dp.
+    (The GPU solver runs all 50 against the same golden in test_gpu_solver.py.)"""
+    d = golden("data_img5.npz")
+    g = golden("lrs_pnp_cfg0_50iter.npz")
+    Y = unfold(d["noisy"][0])
+    M = mask_matrix(d["fourth_mask"], 128)
+    o = O.LrsPnpOracle(Y, M, synthetic_dictionary(1296, 256, 0), bb=36, sliding=36, Nit=80, variant="spec2")
+    clean = d["clean"][0]
+    for it in range(3):
+        o.step()
+        if it < 2:
+            ref = g["X1"] if it == 0 else g["X2"]
+            assert np.linalg.norm(o.X - ref) / np.linalg.norm(ref) < 1e-6
+        assert abs(O.psnr_bands(o.X, clean).mean() - g["mpsnr"][it]) < 1e-4
