@@ -291,6 +291,13 @@ int lrs_dipnet_init_params(lrs_dipnet *net, uint64_t seed, void *stream);
 int lrs_dipnet_reset_optimizer(lrs_dipnet *net, void *stream);
 /* forward only (spectral norms included); the output stays in lrs_dipnet_output() */
 int lrs_dipnet_forward(lrs_dipnet *net, const float *x, void *stream);
+/* backward from gout = dL/d(output) (C x H x W, device) through the activations of the last
+ * lrs_dipnet_forward on the same x: every parameter gradient into the bound grads buffer (sigma
+ * and the BN scale c are constants, as the reference takes them from .data); no input gradient.
+ * Replaces loss.backward() through my_Lipschitz_Unet / skip (…1-LiP.py:237, pro :245). */
+int lrs_dipnet_backward(lrs_dipnet *net, const float *x, const float *gout, void *stream);
+/* ln_lambda of the spectral normalisation (my_Lipschitz_Unet(..., ln_lambda); default 1) */
+int lrs_dipnet_set_ln_lambda(lrs_dipnet *net, float ln_lambda);
 const float *lrs_dipnet_output(const lrs_dipnet *net);
 const float *lrs_dipnet_grads(const lrs_dipnet *net);
 /* nsteps training steps: forward, masked MSE, backward, Adam; es (nullable) gets every step's

@@ -725,6 +725,7 @@ struct lrs_dipnet {
         float lr, b1, b2, eps;
     } key{};
     bool have_key = false;
+    float ln_lambda = 1.0f;   // W_used = W / max(1, sigma / ln_lambda)   (lipschitz_constraint_layer.py:42-44)
 
     float *f(int64_t off) const { return (float *)ws + off; }
     double *gram() const { return (double *)(ws + gram_off_bytes); }
@@ -746,7 +747,7 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
     int rc;
     if (net->n_sn) {
         rc = sn_launch(net->table(), net->n_sn, net->max_w, net->gram(), net->f(net->sigma_off),
-                       net->f(net->scale_off), 1.0f, true, st);
+                       net->f(net->scale_off), net->ln_lambda, true, st);
         if (rc) return rc;
     }
     for (size_t i = 0; i < net->nodes.size(); ++i) {
@@ -782,6 +783,8 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
     return LRS_OK;
 }
 
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st);
+
 int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const float *mask, float lr, float b1, float b2,
                 float eps, lrs_es_state *es, float *ring, hipStream_t st) {
     int rc = dipnet_forward(net, x, st);
@@ -794,6 +797,23 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
     hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, st, net->loss_acc(), net->step());
     rc = lrs_masked_mse_f32(out, target, mask, Lst.C, Lst.P, net->f(Lst.grad_off), net->loss_acc(), st);
     if (rc) return rc;
+    rc = dipnet_backward(net, x, st);
+    if (rc) return rc;
+    rc = lrs_adam_f32(net->params, net->grads, net->am, net->av, net->n_params, net->step(), lr, b1, b2, eps, st);
+    if (rc) return rc;
+    if (es) {
+        rc = es_update(out, (int64_t)Lst.C * Lst.P, ring, es, st);
+        if (rc) return rc;
+    }
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+// Backward from dL/d(output) already in the last node's gradient buffer: every parameter
+// gradient into net->grads (the input gets none: the reference's DIP input needs no gradient).
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st) {
+    int rc;
+    const int n = (int)net->nodes.size();
     // gradient buffers: the first contribution to a tensor writes, later ones accumulate
     std::vector<char> written(n + 1, 0);
     written[n] = 1;
@@ -873,16 +893,10 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
             if (tb > 0) written[tb] = 1;
         }
     }
-    if (net->fork_w) {   // join the side stream before Adam reads the weight gradients
+    if (net->fork_w) {   // join the side stream before anyone reads the weight gradients
         hipError_t e = hipEventRecord(net->ev_join, net->side);
         if (e == hipSuccess) e = hipStreamWaitEvent(st, net->ev_join, 0);
         if (e != hipSuccess) return (int)e;
-    }
-    rc = lrs_adam_f32(net->params, net->grads, net->am, net->av, net->n_params, net->step(), lr, b1, b2, eps, st);
-    if (rc) return rc;
-    if (es) {
-        rc = es_update(out, (int64_t)Lst.C * Lst.P, ring, es, st);
-        if (rc) return rc;
     }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
@@ -1129,6 +1143,26 @@ extern "C" int lrs_dipnet_reset_optimizer(lrs_dipnet *net, void *stream) {
 extern "C" int lrs_dipnet_forward(lrs_dipnet *net, const float *x, void *stream) {
     if (!net || !net->ws || !x) return LRS_E_INVALID;
     return dipnet_forward(net, x, (hipStream_t)stream);
+}
+
+static int ensure_side(lrs_dipnet *net);
+
+extern "C" int lrs_dipnet_backward(lrs_dipnet *net, const float *x, const float *gout, void *stream) {
+    if (!net || !net->ws || !x || !gout) return LRS_E_INVALID;
+    if (const int rs = ensure_side(net)) return rs;
+    hipStream_t st = (hipStream_t)stream;
+    const auto &Lst = net->nodes.back();
+    const hipError_t e = hipMemcpyAsync(net->f(Lst.grad_off), gout, sizeof(float) * Lst.C * Lst.P,
+                                        hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return (int)e;
+    return dipnet_backward(net, x, st);
+}
+
+extern "C" int lrs_dipnet_set_ln_lambda(lrs_dipnet *net, float ln_lambda) {
+    if (!net || !(ln_lambda > 0.0f)) return LRS_E_INVALID;
+    drop_graph(net);
+    net->ln_lambda = ln_lambda;
+    return LRS_OK;
 }
 
 extern "C" const float *lrs_dipnet_output(const lrs_dipnet *net) {

@@ -141,7 +141,9 @@ def _check(rc, what):
 class DipNet:
     """A sequential conv net on the HIP engine (lrs_dipnet_*), with flat parameter buffers."""
 
-    def __init__(self, nodes: list[DipNode], C: int, H: int, W: int, device="cuda"):
+    def __init__(self, nodes: list[DipNode], C: int, H: int, W: int, device="cuda", params=None, bnstats=None):
+        """params / bnstats (optional): existing flat device buffers to bind (shared with another
+        engine of the same nodes at another H x W: the parameter layout does not depend on it)."""
         import torch
 
         self.L = _lib.device_lib()
@@ -155,11 +157,13 @@ class DipNet:
         nbs = int(self.L.lrs_dipnet_num_bnstats(h))
         ws = int(self.L.lrs_dipnet_workspace(h))
         f32 = dict(dtype=torch.float32, device=device)
-        self.params = torch.zeros(self.n_params, **f32)
+        if params is not None and (params.numel() != self.n_params or params.dtype != torch.float32 or not params.is_cuda):
+            raise _lib.LrsError(f"shared params must be {self.n_params} float32 on the device")
+        self.params = params if params is not None else torch.zeros(self.n_params, **f32)
         self.grads = torch.zeros(self.n_params, **f32)
         self.exp_avg = torch.zeros(self.n_params, **f32)
         self.exp_avg_sq = torch.zeros(self.n_params, **f32)
-        self.bnstats = torch.zeros(max(nbs, 1), **f32)
+        self.bnstats = bnstats if bnstats is not None else torch.zeros(max(nbs, 1), **f32)
         self.ws = torch.zeros(ws, dtype=torch.uint8, device=device)
         _check(self.L.lrs_dipnet_bind(h, _ptr(self.params), _ptr(self.grads), _ptr(self.exp_avg),
                                       _ptr(self.exp_avg_sq), _ptr(self.bnstats), _ptr(self.ws), ws),
@@ -243,6 +247,19 @@ class DipNet:
                "lrs_dipnet_forward")
         torch.cuda.current_stream().wait_stream(self.stream)
         return self.output()
+
+    def backward(self, x, gout):
+        """Parameter gradients (into self.grads) of the last forward(x) for dL/dout = gout."""
+        import torch
+        x, gout = x.contiguous(), gout.contiguous()
+        assert tuple(gout.shape[-3:]) == self.out_shape and gout.dtype == torch.float32 and gout.is_cuda
+        self.stream.wait_stream(torch.cuda.current_stream())
+        _check(self.L.lrs_dipnet_backward(self.h, _ptr(x), _ptr(gout), ctypes.c_void_p(self.stream.cuda_stream)),
+               "lrs_dipnet_backward")
+        torch.cuda.current_stream().wait_stream(self.stream)
+
+    def set_ln_lambda(self, ln_lambda: float):
+        _check(self.L.lrs_dipnet_set_ln_lambda(self.h, ctypes.c_float(ln_lambda)), "lrs_dipnet_set_ln_lambda")
 
     def output(self):
         import torch
