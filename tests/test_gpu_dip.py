@@ -489,6 +489,34 @@ def test_skip_net_generalised_bands(L):
     assert rel(out, dip_ref.forward(flat, nodes, x)) < 1e-5
 
 
+def test_skip_net_config3_full_size(L):
+    """BASELINE configs[3]'s DIP at full size: the skip net (5 x 128 channels, 128-ch skips, Sigmoid)
+    on a 512 x 512 x 224 cube (main_LRS_PnP_DIP_pro.py:215-221 with 224 bands): the engine's forward
+    against the plain-torch fp32 restatement run on the GPU (TF32 off) at 1e-5 relative L2, and the
+    step-0 masked-MSE loss at 1e-5."""
+    from gen_dip_golden import flat_params
+    from lrspnp.dip import skip_nodes
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    C, H = 224, 512
+    nodes = skip_nodes(C, C)
+    flat = torch.from_numpy(flat_params(nodes, 11, C, H, H))
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(C, H, H, generator=g)
+    t = torch.rand(C, H, H, generator=g)
+    m = (torch.rand(H * H, generator=g) > 0.05).float()
+    net = _engine(nodes, flat, H, H, C)
+    out = net.forward(x.cuda())
+    with torch.no_grad():
+        ref = dip_ref.forward(flat.cuda(), nodes, x.cuda())
+        loss_r = float(dip_ref.loss_fn(ref, t.cuda(), m.cuda()))
+    assert out.shape == ref.shape == (C, H, H)
+    assert rel(out, ref) < 1e-5
+    net.train_steps(x.cuda(), t.cuda(), m.cuda(), 1, use_graph=False)
+    torch.cuda.synchronize()
+    assert abs(net.last_loss() - loss_r) < 1e-5 * loss_r
+
+
 def test_solver_dip_pro_skip_runs(L, golden):
     """One LRS-PnP-DIP(pro) outer iteration: the skip net as the low-rank prox (…pro.py:399-420)."""
     from lrspnp import LrsPnP, LrsPnPConfig
