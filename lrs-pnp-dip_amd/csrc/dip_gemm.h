@@ -604,6 +604,49 @@ __global__ __launch_bounds__(256) void k_wprep(const float *__restrict__ W, int 
     }
 }
 
+// Per-step weight preparation of every conv of a network in ONE launch (grid (blocks, convs)):
+// Wn = W_bar / scale[si] for the spectrally normalised convs (lipschitz_constraint_layer.py:42-44)
+// and the bf16 planes of k_wprep (forward WF, data-gradient WD) of the convs that run on the
+// split-bf16 kernels, from the same W / scale quotient.
+struct ConvPrep {
+    const float *W;
+    float *Wn;          // nullable
+    __bf16 *wf, *wd;    // nullable
+    int Cout, Cin, kk, Cp, Cop, si;   // si: scale index, -1 = no spectral norm
+};
+
+__global__ __launch_bounds__(256) void k_conv_prep(const ConvPrep *__restrict__ tab, const float *__restrict__ scale) {
+    const ConvPrep c = tab[blockIdx.y];
+    const float s = c.si >= 0 ? scale[c.si] : 1.0f;
+    const int64_t nw = (int64_t)c.Cout * c.Cin * c.kk;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x, i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c.Wn)
+        for (int64_t i = i0; i < nw; i += stride) c.Wn[i] = c.W[i] / s;
+    const int64_t nf = c.wf ? (int64_t)c.Cout * c.kk * c.Cp : 0, nd = c.wd ? (int64_t)c.Cin * c.kk * c.Cop : 0;
+    for (int64_t i = i0; i < nf + nd; i += stride) {
+        float x;
+        __bf16 *dst;
+        int64_t plane, j;
+        if (i < nf) {
+            const int co = (int)(i / (c.kk * c.Cp)), rem = (int)(i - (int64_t)co * c.kk * c.Cp);
+            const int kyx = rem / c.Cp, ci = rem - kyx * c.Cp;
+            x = ci < c.Cin ? c.W[((int64_t)co * c.Cin + ci) * c.kk + kyx] : 0.0f;
+            dst = c.wf; plane = nf; j = i;
+        } else {
+            j = i - nf;
+            const int ci = (int)(j / (c.kk * c.Cop)), rem = (int)(j - (int64_t)ci * c.kk * c.Cop);
+            const int kyx = rem / c.Cop, co = rem - kyx * c.Cop;
+            x = co < c.Cout ? c.W[((int64_t)co * c.Cin + ci) * c.kk + kyx] : 0.0f;
+            dst = c.wd; plane = nd;
+        }
+        if (c.si >= 0) x = x / s;
+        const S3Split q = s3_split(x);
+        dst[j] = q.b0;
+        dst[plane + j] = q.b1;
+        dst[2 * plane + j] = q.b2;
+    }
+}
+
 // gx[c][sy][sx] (+)= sum over the x2 upsample children u of sum over the padded positions that
 // read u (direct + reflection mirrors, padded_sources) of gxp[c][iy][ix]
 __global__ __launch_bounds__(256) void k_fold_pad(const float *__restrict__ gxp, ConvGeom gm, float *__restrict__ gx,

@@ -702,7 +702,8 @@ struct lrs_dipnet {
     int C0 = 0, H = 0, W = 0;
     int64_t n_params = 0, n_bnstats = 0;
     int64_t dz_off = 0, dcol_off = 0, part_off = 0, part_cap = 0, sigma_off = 0, scale_off = 0;
-    int64_t gram_off_bytes = 0, table_off_bytes = 0, misc_off_bytes = 0, bnpart_off_bytes = 0;
+    int64_t gram_off_bytes = 0, table_off_bytes = 0, misc_off_bytes = 0, bnpart_off_bytes = 0, prep_off_bytes = 0;
+    int n_prep = 0;           // convs in the per-step weight-preparation table (spectral norm and/or planes)
     size_t ws_bytes = 0;
     int n_sn = 0;
     int64_t max_w = 0;
@@ -730,6 +731,7 @@ struct lrs_dipnet {
     float *f(int64_t off) const { return (float *)ws + off; }
     double *gram() const { return (double *)(ws + gram_off_bytes); }
     SnConv *table() const { return (SnConv *)(ws + table_off_bytes); }
+    ConvPrep *prep() const { return (ConvPrep *)(ws + prep_off_bytes); }
     double *loss_acc() const { return (double *)(ws + misc_off_bytes); }
     int *step() const { return (int *)(ws + misc_off_bytes + 8); }
     double *bnpart() const { return (double *)(ws + bnpart_off_bytes); }
@@ -747,8 +749,12 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
     int rc;
     if (net->n_sn) {
         rc = sn_launch(net->table(), net->n_sn, net->max_w, net->gram(), net->f(net->sigma_off),
-                       net->f(net->scale_off), net->ln_lambda, true, st);
+                       net->f(net->scale_off), net->ln_lambda, false, st);
         if (rc) return rc;
+    }
+    if (net->n_prep) {   // W / scale and the bf16 planes of every conv, one launch
+        hipLaunchKernelGGL(k_conv_prep, dim3(128, net->n_prep), dim3(256), 0, st, net->prep(), net->f(net->scale_off));
+        LRS_CHECK_LAUNCH();
     }
     for (size_t i = 0; i < net->nodes.size(); ++i) {
         auto &N = net->nodes[i];
@@ -759,7 +765,6 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
             float *z = bn ? net->f(N.z_off) : out;
             const float *w = N.sn_index >= 0 ? net->f(N.wn_off) : net->params + N.w_off;
             __bf16 *wp = N.wpre_off >= 0 ? (__bf16 *)net->f(N.wpre_off) : nullptr;
-            if (wp) wprep(N.g, w, N.C, wp, N.d.in0 > 0 ? wp + wprep_fwd_elems(N.g, N.C) : nullptr, st);
             rc = conv_fwd(N.g, net->tensor(N.d.in0, x), w, net->params + N.b_off, N.C,
                           N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st, wp);
             if (rc) return rc;
@@ -1031,6 +1036,10 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     bytes += (size_t)round_up((max_bnpart > 0 ? max_bnpart : 1) * (int64_t)sizeof(double), 256);
     net->table_off_bytes = (int64_t)bytes;
     bytes += (size_t)round_up((int64_t)((n_sn > 0 ? n_sn : 1) * sizeof(SnConv)), 256);
+    for (const auto &N : net->nodes)
+        if (N.d.kind == LRS_NODE_CONV && (N.sn_index >= 0 || N.wpre_off >= 0)) ++net->n_prep;
+    net->prep_off_bytes = (int64_t)bytes;
+    bytes += (size_t)round_up((int64_t)((net->n_prep > 0 ? net->n_prep : 1) * sizeof(ConvPrep)), 256);
     net->misc_off_bytes = (int64_t)bytes;
     bytes += 256;
     net->ws_bytes = bytes;
@@ -1093,8 +1102,19 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
     std::vector<SnConv> tab;
     for (const auto &N : net->nodes)
         if (N.sn_index >= 0) tab.push_back(SnConv{params + N.w_off, net->f(N.wn_off), N.C, (int)N.Kc});
+    std::vector<ConvPrep> prep;
+    for (size_t i = 0; i < net->nodes.size(); ++i) {
+        const auto &N = net->nodes[i];
+        if (N.d.kind != LRS_NODE_CONV || (N.sn_index < 0 && N.wpre_off < 0)) continue;
+        __bf16 *wf = N.wpre_off >= 0 ? (__bf16 *)net->f(N.wpre_off) : nullptr;
+        __bf16 *wd = (wf && N.d.in0 > 0) ? wf + wprep_fwd_elems(N.g, N.C) : nullptr;
+        prep.push_back(ConvPrep{params + N.w_off, N.sn_index >= 0 ? net->f(N.wn_off) : nullptr, wf, wd, N.C, N.g.Cin,
+                                N.g.k * N.g.k, r16(N.g.Cin), r16(N.C), N.sn_index});
+    }
     hipError_t e = hipSuccess;
     if (!tab.empty()) e = hipMemcpy(net->table(), tab.data(), sizeof(SnConv) * tab.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !prep.empty())
+        e = hipMemcpy(net->prep(), prep.data(), sizeof(ConvPrep) * prep.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(net->misc_off_bytes + net->ws, 0, 256);
     return e == hipSuccess ? LRS_OK : (int)e;
 }
