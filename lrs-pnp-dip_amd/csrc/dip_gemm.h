@@ -615,7 +615,12 @@ struct ConvPrep {
     int Cout, Cin, kk, Cp, Cop, si;   // si: scale index, -1 = no spectral norm
 };
 
-__global__ __launch_bounds__(256) void k_conv_prep(const ConvPrep *__restrict__ tab, const float *__restrict__ scale) {
+__global__ __launch_bounds__(256) void k_conv_prep(const ConvPrep *__restrict__ tab, const float *__restrict__ scale,
+                                                   double *loss_acc, int *step) {
+    if (loss_acc && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {   // a training step begins
+        *loss_acc = 0.0;
+        *step += 1;
+    }
     const ConvPrep c = tab[blockIdx.y];
     const float s = c.si >= 0 ? scale[c.si] : 1.0f;
     const int64_t nw = (int64_t)c.Cout * c.Cin * c.kk;

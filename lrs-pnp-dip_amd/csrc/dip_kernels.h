@@ -1244,6 +1244,72 @@ __global__ __launch_bounds__(256) void k_masked_mse(const float *__restrict__ ou
     if (threadIdx.x == 0) atomicAdd(loss_acc, s);
 }
 
+// Loss head of a training step whose last node is a conv without BN (both reference nets): the
+// masked MSE (as k_masked_mse: loss_acc += sum d^2, dL/dout = -(2/(C P)) d m) fused with that
+// node's activation backward dL/dz = act'(out) dL/dout and its bias gradient sum_p dL/dz: one pass
+// instead of masked-MSE + BN-backward statistics + BN-backward apply.  Bias partials [c][chunk]
+// (fp64) are summed in chunk order by the last workgroup of each channel to finish (a per-channel
+// counter, reset by that workgroup), so the bias gradient is deterministic.
+__global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out, const float *__restrict__ target,
+                                                  const float *__restrict__ mask, int C, int64_t P, int chunk,
+                                                  int vec, int act, float *__restrict__ gz, double *loss_acc,
+                                                  double *__restrict__ bpart, int *__restrict__ cnt,
+                                                  float *__restrict__ gbias) {
+    __shared__ double red[8];
+    __shared__ int last;
+    const float norm = (float)(2.0 / ((double)C * (double)P));
+    const int c = blockIdx.y;
+    const int64_t off = (int64_t)c * P;
+    const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(P, i0 + chunk);
+    double s = 0.0, sb = 0.0;
+    if (vec) {
+        const float4 *o4 = reinterpret_cast<const float4 *>(out + off), *t4 = reinterpret_cast<const float4 *>(target + off);
+        const float4 *m4 = reinterpret_cast<const float4 *>(mask);
+        float4 *g4 = reinterpret_cast<float4 *>(gz + off);
+        for (int64_t q = (i0 >> 2) + threadIdx.x; q < (i1 >> 2); q += blockDim.x) {
+            const float4 ov = o4[q], tv = t4[q];
+            const float4 mv = mask ? m4[q] : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+            const float oe[4] = {ov.x, ov.y, ov.z, ov.w}, te[4] = {tv.x, tv.y, tv.z, tv.w},
+                        me[4] = {mv.x, mv.y, mv.z, mv.w};
+            float ge[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = te[e] * me[e] - oe[e] * me[e];
+                s += (double)d * (double)d;
+                ge[e] = act_bwd((-(norm * d)) * me[e], oe[e], act);
+                sb += (double)ge[e];
+            }
+            g4[q] = make_float4(ge[0], ge[1], ge[2], ge[3]);
+        }
+    } else {
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+            const float mk = mask ? mask[i] : 1.0f;
+            const float o = out[off + i];
+            const float d = target[off + i] * mk - o * mk;
+            s += (double)d * (double)d;
+            const float g = act_bwd((-(norm * d)) * mk, o, act);
+            gz[off + i] = g;
+            sb += (double)g;
+        }
+    }
+    s = block_sum_d(s, red);
+    if (threadIdx.x == 0) atomicAdd(loss_acc, s);
+    sb = block_sum_d(sb, red);
+    if (threadIdx.x == 0) {
+        bpart[(int64_t)c * gridDim.x + blockIdx.x] = sb;
+        __threadfence();
+        last = atomicAdd(cnt + c, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        double t = 0.0;
+        for (unsigned k = 0; k < gridDim.x; ++k) t += bpart[(int64_t)c * gridDim.x + k];
+        gbias[c] = (float)t;
+        cnt[c] = 0;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Adam (torch.optim.Adam defaults: no weight decay, no amsgrad), flat parameter buffer.
 // step is a device counter so a captured step replays correctly.

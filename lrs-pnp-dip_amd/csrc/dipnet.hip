@@ -704,6 +704,8 @@ struct lrs_dipnet {
     int64_t dz_off = 0, dcol_off = 0, part_off = 0, part_cap = 0, sigma_off = 0, scale_off = 0;
     int64_t gram_off_bytes = 0, table_off_bytes = 0, misc_off_bytes = 0, bnpart_off_bytes = 0, prep_off_bytes = 0;
     int n_prep = 0;           // convs in the per-step weight-preparation table (spectral norm and/or planes)
+    int64_t headcnt_off_bytes = 0;   // per-channel counters of k_mse_head (zeroed at bind, reset by the kernel)
+    bool head_fusable = false;       // last node = conv without BN: loss + its activation backward in one kernel
     size_t ws_bytes = 0;
     int n_sn = 0;
     int64_t max_w = 0;
@@ -732,6 +734,7 @@ struct lrs_dipnet {
     double *gram() const { return (double *)(ws + gram_off_bytes); }
     SnConv *table() const { return (SnConv *)(ws + table_off_bytes); }
     ConvPrep *prep() const { return (ConvPrep *)(ws + prep_off_bytes); }
+    int *headcnt() const { return (int *)(ws + headcnt_off_bytes); }
     double *loss_acc() const { return (double *)(ws + misc_off_bytes); }
     int *step() const { return (int *)(ws + misc_off_bytes + 8); }
     double *bnpart() const { return (double *)(ws + bnpart_off_bytes); }
@@ -745,7 +748,7 @@ namespace {
 
 int64_t align64(int64_t n) { return (n + 63) / 64 * 64; }   // floats (256 bytes)
 
-int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
+int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_begin = false) {
     int rc;
     if (net->n_sn) {
         rc = sn_launch(net->table(), net->n_sn, net->max_w, net->gram(), net->f(net->sigma_off),
@@ -753,7 +756,8 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
         if (rc) return rc;
     }
     if (net->n_prep) {   // W / scale and the bf16 planes of every conv, one launch
-        hipLaunchKernelGGL(k_conv_prep, dim3(128, net->n_prep), dim3(256), 0, st, net->prep(), net->f(net->scale_off));
+        hipLaunchKernelGGL(k_conv_prep, dim3(128, net->n_prep), dim3(256), 0, st, net->prep(), net->f(net->scale_off),
+                           step_begin ? net->loss_acc() : nullptr, net->step());
         LRS_CHECK_LAUNCH();
     }
     for (size_t i = 0; i < net->nodes.size(); ++i) {
@@ -788,21 +792,46 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st) {
     return LRS_OK;
 }
 
-int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st);
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done = false);
+int mse_head(lrs_dipnet *net, const float *out, const float *target, const float *mask, hipStream_t st);
+
+// k_mse_head over the last node (conv without BN): gz and the bias gradient of that node, + loss
+int mse_head(lrs_dipnet *net, const float *out, const float *target, const float *mask, hipStream_t st) {
+    const auto &N = net->nodes.back();
+    float *gz = net->f(N.gz_off);
+    const int64_t P = N.P;
+    const int vec = (P % 4 == 0 && al16(out) && al16(target) && (!mask || al16(mask)) && al16(gz)) ? 1 : 0;
+    int64_t S = (512 + N.C - 1) / N.C;
+    S = std::max<int64_t>(1, std::min<int64_t>(S, (P + 1023) / 1024));
+    int64_t chunk = (P + S - 1) / S;
+    if (vec) chunk = (chunk + 3) & ~(int64_t)3;
+    S = (P + chunk - 1) / chunk;
+    if (chunk > INT32_MAX || (int64_t)N.C * S > bn_part_doubles(N.C, P)) return LRS_E_UNSUPPORTED;
+    hipLaunchKernelGGL(k_mse_head, dim3((unsigned)S, (unsigned)N.C), dim3(256), 0, st, out, target, mask, N.C, P,
+                       (int)chunk, vec, N.d.act, gz, net->loss_acc(), net->bnpart(), net->headcnt(),
+                       net->grads + N.b_off);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
 
 int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const float *mask, float lr, float b1, float b2,
                 float eps, lrs_es_state *es, float *ring, hipStream_t st) {
-    int rc = dipnet_forward(net, x, st);
+    // the weight-preparation launch at the head of the forward also zeroes the loss accumulator
+    // and advances Adam's step counter (read only by this step's k_adam); without one, a tiny launch
+    const bool folded = net->n_prep > 0;
+    int rc = dipnet_forward(net, x, st, folded);
     if (rc) return rc;
     const int n = (int)net->nodes.size();
     const auto &Lst = net->nodes[n - 1];
     const float *out = net->f(Lst.out_off);
-    // one tiny launch zeroes the loss accumulator and advances Adam's step counter (read only by
-    // this step's k_adam)
-    hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, st, net->loss_acc(), net->step());
-    rc = lrs_masked_mse_f32(out, target, mask, Lst.C, Lst.P, net->f(Lst.grad_off), net->loss_acc(), st);
+    if (!folded) hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, st, net->loss_acc(), net->step());
+    if (net->head_fusable) {
+        rc = mse_head(net, out, target, mask, st);
+    } else {
+        rc = lrs_masked_mse_f32(out, target, mask, Lst.C, Lst.P, net->f(Lst.grad_off), net->loss_acc(), st);
+    }
     if (rc) return rc;
-    rc = dipnet_backward(net, x, st);
+    rc = dipnet_backward(net, x, st, net->head_fusable);
     if (rc) return rc;
     rc = lrs_adam_f32(net->params, net->grads, net->am, net->av, net->n_params, net->step(), lr, b1, b2, eps, st);
     if (rc) return rc;
@@ -816,7 +845,7 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
 
 // Backward from dL/d(output) already in the last node's gradient buffer: every parameter
 // gradient into net->grads (the input gets none: the reference's DIP input needs no gradient).
-int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st) {
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done) {
     int rc;
     const int n = (int)net->nodes.size();
     // gradient buffers: the first contribution to a tensor writes, later ones accumulate
@@ -832,10 +861,13 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st) {
             const bool bn = N.d.bn != 0;
             float *z = bn ? net->f(N.z_off) : outp;
             float *gz = net->f(N.gz_off);
-            rc = bn_bwd(gout, outp, z, bn ? net->params + N.gm_off : nullptr, net->f(N.mean_off), net->f(N.istd_off),
-                        gz, bn ? net->grads + N.gm_off : nullptr, bn ? net->grads + N.bt_off : nullptr,
-                        net->grads + N.b_off, N.C, N.P, N.d.act, net->bnpart(), st, lip, 0);
-            if (rc) return rc;
+            if (!(head_done && i == n - 1)) {   // else k_mse_head wrote gz and the bias gradient
+                rc = bn_bwd(gout, outp, z, bn ? net->params + N.gm_off : nullptr, net->f(N.mean_off),
+                            net->f(N.istd_off), gz, bn ? net->grads + N.gm_off : nullptr,
+                            bn ? net->grads + N.bt_off : nullptr, net->grads + N.b_off, N.C, N.P, N.d.act,
+                            net->bnpart(), st, lip, 0);
+                if (rc) return rc;
+            }
             const int t = N.d.in0;
             const float *colsrc = N.col_off >= 0 ? net->f(N.col_off) : net->tensor(t, x);
             const bool sn = N.sn_index >= 0;
@@ -1040,6 +1072,10 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
         if (N.d.kind == LRS_NODE_CONV && (N.sn_index >= 0 || N.wpre_off >= 0)) ++net->n_prep;
     net->prep_off_bytes = (int64_t)bytes;
     bytes += (size_t)round_up((int64_t)((net->n_prep > 0 ? net->n_prep : 1) * sizeof(ConvPrep)), 256);
+    net->head_fusable = net->nodes.back().d.kind == LRS_NODE_CONV && net->nodes.back().d.bn == 0 &&
+                        net->nodes.back().C <= 65535;
+    net->headcnt_off_bytes = (int64_t)bytes;
+    bytes += (size_t)round_up((int64_t)net->nodes.back().C * 4, 256);
     net->misc_off_bytes = (int64_t)bytes;
     bytes += 256;
     net->ws_bytes = bytes;
@@ -1116,6 +1152,7 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
     if (e == hipSuccess && !prep.empty())
         e = hipMemcpy(net->prep(), prep.data(), sizeof(ConvPrep) * prep.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(net->misc_off_bytes + net->ws, 0, 256);
+    if (e == hipSuccess) e = hipMemset(net->headcnt(), 0, sizeof(int) * net->nodes.back().C);
     return e == hipSuccess ? LRS_OK : (int)e;
 }
 
