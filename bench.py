@@ -20,8 +20,9 @@ Multi-GPU (one process per GPU, RCCL): one independent cube per rank (seed = ran
 collective (SURVEY.md §8e); barrier + synchronize around the K timed steps, MAX over ranks;
 value = ranks * K / max_time ("weak").  `--gpus N` without a torchrun environment starts N ranks
 itself (a child torch.distributed.run, before any GPU call); a rank count that differs from
---gpus is an error.  pnp only: --split-cube runs ONE cube over the ranks in pixel-row slabs with an
-fp64 all-reduce of the B x B SVT Gram per iteration ("strong").
+--gpus is an error.  --split-cube runs ONE cube over the ranks ("strong"): pnp in pixel-row slabs
+with an fp64 all-reduce of the B x B SVT Gram per iteration; dip / dip-pro task-parallel (DIP on
+rank 0, the sparse coding's blocks over the other ranks, U broadcast + Phi all-gathered).
 
 Rank 0 prints one JSON line with
   roofline     : the dominant stage — the DIP training of one outer iteration (dip workloads) or
@@ -70,15 +71,14 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group: nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
     ap.add_argument("--split-cube", action="store_true",
-                    help="pnp only: one cube over all ranks in pixel-row slabs (strong scaling)")
+                    help="one cube over all ranks (strong scaling): pnp in pixel-row slabs; dip task-parallel "
+                         "(DIP on rank 0, sparse coding over the others)")
     a = ap.parse_args()
     dip = a.workload != "pnp"
     if a.steps is None:
         a.steps = 3 if dip else 10
     if a.warmup is None:
         a.warmup = 1 if dip else 2
-    if a.split_cube and dip:
-        ap.error("--split-cube applies to --workload pnp only (the DIP trains on the whole image)")
     return a
 
 
@@ -266,10 +266,12 @@ def main_dip(args, ctx):
     H, W, B = (int(v) for v in args.cube.split("x")) if args.cube else ((512, 512, 224) if pro else (196, 196, 198))
     bb = args.bb or 36
     nit = args.nit or 100
-    Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=ctx.rank)
+    split = args.split_cube
+    Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=0 if split else ctx.rank)
     dcfg = DipConfig(num_iter=args.dip_steps, early_stop=False, net="skip" if pro else "unet1lip")
     cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, Nit=nit, dip=dcfg)
-    s = LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
+    task = D.DipTaskSplit(Y, M, Dct, cfg, ctx, image_shape=(H, W)) if split else None
+    s = task.s if split else LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
     clean_d = torch.from_numpy(clean).cuda()
     mp0 = mpsnr(s.X, clean_d)
 
@@ -282,12 +284,17 @@ def main_dip(args, ctx):
     def step():
         dip_t.on = ista_t.on = count[0] >= args.warmup
         count[0] += 1
-        s.step()
+        (task.step if split else s.step)()
 
     elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
     ops.ista = orig_ista
     mp1 = mpsnr(s.X, clean_d)
     dip_ms, ista_ms = dip_t.mean_ms(), ista_t.mean_ms()
+    if split and ctx.world > 1:   # rank 0 trained the DIP, ranks 1.. coded: take each stage from those ranks
+        per = D.gather_scalars([dip_ms, ista_ms], ctx)
+        if per is not None:
+            dip_ms = per[0][0]
+            ista_ms = float(np.nanmean([v[1] for v in per[1:]]))
     flops = dip_flops_per_step(s.dip.net) * args.dip_steps
     achieved = flops / (dip_ms * 1e-3) / 1e12
     n = bb * bb
@@ -295,9 +302,9 @@ def main_dip(args, ctx):
     net_desc = ("skip net (5 x 128 ch, 128-ch skips)" if pro else f"my_Lipschitz_Unet ({B}->128->{B} ch)")
     tag = "dip_pro" if pro else "dip"
     out = {
-        "metric": METRIC, "value": ctx.world * args.steps / elapsed, "unit": "outer_iters/s",
+        "metric": METRIC, "value": (1 if split else ctx.world) * args.steps / elapsed, "unit": "outer_iters/s",
         "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong" if split else "weak",
         "vs_baseline": None, "dtype": "f32 (MFMA products fp32-accurate) + f64 (NLM prox, BN/sigma statistics)",
         "data": f"synthetic (seeded low-rank {H}x{W}x{B} cube per rank, tiled low_rank_sparsity_mask, seeded "
                 f"K={args.K} dictionary, random-init DIP net per outer iteration)",
@@ -307,7 +314,9 @@ def main_dip(args, ctx):
                                 f"(BASELINE configs[2]; 196 = largest 16a-12 size <= 200 that the U-Net maps onto "
                                 f"itself)") + f": {bb}x{bb} blocks ({s.nb}), K={args.K}, Nit={nit} fro4 ISTA + NLM "
                                f"prox; DIP {net_desc} {args.dip_steps} Adam steps per outer iteration, ES off",
-                   "blocks": s.nb, "parallelism": f"{ctx.world} independent cube(s), one per GPU"},
+                   "blocks": s.nb,
+                   "parallelism": (f"1 cube, task-parallel: DIP on rank 0, sparse coding over {ctx.world - 1} rank(s)"
+                                   if split and ctx.world > 1 else f"{ctx.world} independent cube(s), one per GPU")},
         "roofline": {"bound": "mfma", "kernel": f"DIP training of one outer iteration ({args.dip_steps} steps: conv "
                                                 f"GEMMs, sigma_max, BN, loss, Adam kernels)",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",

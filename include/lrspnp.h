@@ -122,6 +122,12 @@ int lrs_ista_get_precision(void);
 #define LRS_DIP_SPLIT_BF16 1
 int lrs_dip_set_precision(int precision);
 int lrs_dip_get_precision(void);
+/* Data gradient of an upsampled stride-1 conv (nearest x2, then 2x2 unpadded or 3x3 pad 1):
+ * 0 (default) = correlation over the padded upsampled domain + fold; 1 = a stride-2 conv with the
+ * (k+1)x(k+1) effective kernel on the source grid (2.25x fewer products) + reflection border
+ * terms.  Process-wide; a lrs_dipnet fixes its layout at creation, the lrs_conv2d_* workspace
+ * sizes follow the current mode. */
+int lrs_dip_set_upsample_dgrad(int mode);
 
 /* ---- SVT low-rank prox ---------------------------------------------------------------------
  * U = SVT(Z, tau) with Z = X + c2 * L2 (c2 = float(1/mu_2); L2 may be NULL), via an fp64 Gram

@@ -330,7 +330,7 @@ struct HasPrepare<LdWgradTM> {
     static constexpr bool value = true;
 };
 
-constexpr int kS3TabInts = 9 * 128;   // k <= 3
+constexpr int kS3TabInts = 16 * 128;  // k <= 4 (the 4 x 4 effective kernel of an upsampled 3 x 3 conv's data gradient)
 
 template <class LA, class LB>
 __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
@@ -575,59 +575,28 @@ __global__ __launch_bounds__(256) void k_pw(PwArgs a) {
     }
 }
 
-// Per conv weight W [Cout][Cin][kk] (fp32): the three bf16 planes of the forward operand
-// WF[p][co][kyx * Cp + c] and of the data-gradient operand WD[p][ci][kyx * Cop + co]
-// (Cp, Cop: Cin, Cout rounded up to 16; padding zero).  WD nullable.
-__global__ __launch_bounds__(256) void k_wprep(const float *__restrict__ W, int Cout, int Cin, int kk, int Cp, int Cop,
-                                               __bf16 *__restrict__ WF, __bf16 *__restrict__ WD) {
-    const int64_t nf = (int64_t)Cout * kk * Cp, nd = WD ? (int64_t)Cin * kk * Cop : 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf + nd; i += (int64_t)gridDim.x * blockDim.x) {
-        float x;
-        __bf16 *dst;
-        int64_t plane, j;
-        if (i < nf) {
-            const int co = (int)(i / (kk * Cp)), rem = (int)(i - (int64_t)co * kk * Cp);
-            const int kyx = rem / Cp, c = rem - kyx * Cp;
-            x = c < Cin ? W[((int64_t)co * Cin + c) * kk + kyx] : 0.0f;
-            dst = WF; plane = nf; j = i;
-        } else {
-            j = i - nf;
-            const int ci = (int)(j / (kk * Cop)), rem = (int)(j - (int64_t)ci * kk * Cop);
-            const int kyx = rem / Cop, co = rem - kyx * Cop;
-            x = co < Cout ? W[((int64_t)co * Cin + ci) * kk + kyx] : 0.0f;
-            dst = WD; plane = nd;
-        }
-        const S3Split q = s3_split(x);
-        dst[j] = q.b0;
-        dst[plane + j] = q.b1;
-        dst[2 * plane + j] = q.b2;
-    }
-}
-
 // Per-step weight preparation of every conv of a network in ONE launch (grid (blocks, convs)):
 // Wn = W_bar / scale[si] for the spectrally normalised convs (lipschitz_constraint_layer.py:42-44)
-// and the bf16 planes of k_wprep (forward WF, data-gradient WD) of the convs that run on the
-// split-bf16 kernels, from the same W / scale quotient.
+// and the bf16 planes the split-bf16 kernels read, from the same W / scale quotient:
+//   WF[p][co][kyx * Cp + ci]            forward operand (Cp = Cin rounded up to 16)
+//   WD[p][ci][kyx * Cop + co]           data-gradient operand (W^T, Cop = Cout rounded up to 16), or,
+//                                       for an upsampled stride-1 conv (ke > 0),
+//   WE[p][ci][(ey * ke + ex) * Cop + co] the effective ke x ke kernel of its data gradient as a
+//                                       stride-2 conv over dL/dz (conv_bwd): the sum of the taps
+//                                       W[a + k-1-ey][b + k-1-ex] over the 2 x 2 upsample children a, b
 struct ConvPrep {
     const float *W;
     float *Wn;          // nullable
-    __bf16 *wf, *wd;    // nullable
-    int Cout, Cin, kk, Cp, Cop, si;   // si: scale index, -1 = no spectral norm
+    __bf16 *wf, *wd;    // nullable (wd holds WE when ke > 0)
+    int Cout, Cin, kk, Cp, Cop, si, k, ke;   // si: scale index, -1 = no spectral norm
 };
 
-__global__ __launch_bounds__(256) void k_conv_prep(const ConvPrep *__restrict__ tab, const float *__restrict__ scale,
-                                                   double *loss_acc, int *step) {
-    if (loss_acc && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {   // a training step begins
-        *loss_acc = 0.0;
-        *step += 1;
-    }
-    const ConvPrep c = tab[blockIdx.y];
-    const float s = c.si >= 0 ? scale[c.si] : 1.0f;
+__device__ __forceinline__ void conv_prep_body(const ConvPrep &c, float s, int64_t i0, int64_t stride) {
     const int64_t nw = (int64_t)c.Cout * c.Cin * c.kk;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x, i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c.Wn)
         for (int64_t i = i0; i < nw; i += stride) c.Wn[i] = c.W[i] / s;
-    const int64_t nf = c.wf ? (int64_t)c.Cout * c.kk * c.Cp : 0, nd = c.wd ? (int64_t)c.Cin * c.kk * c.Cop : 0;
+    const int ed = c.ke > 0 ? c.ke * c.ke : c.kk;
+    const int64_t nf = c.wf ? (int64_t)c.Cout * c.kk * c.Cp : 0, nd = c.wd ? (int64_t)c.Cin * ed * c.Cop : 0;
     for (int64_t i = i0; i < nf + nd; i += stride) {
         float x;
         __bf16 *dst;
@@ -636,20 +605,150 @@ __global__ __launch_bounds__(256) void k_conv_prep(const ConvPrep *__restrict__ 
             const int co = (int)(i / (c.kk * c.Cp)), rem = (int)(i - (int64_t)co * c.kk * c.Cp);
             const int kyx = rem / c.Cp, ci = rem - kyx * c.Cp;
             x = ci < c.Cin ? c.W[((int64_t)co * c.Cin + ci) * c.kk + kyx] : 0.0f;
+            if (c.si >= 0) x = x / s;
             dst = c.wf; plane = nf; j = i;
         } else {
             j = i - nf;
-            const int ci = (int)(j / (c.kk * c.Cop)), rem = (int)(j - (int64_t)ci * c.kk * c.Cop);
-            const int kyx = rem / c.Cop, co = rem - kyx * c.Cop;
-            x = co < c.Cout ? c.W[((int64_t)co * c.Cin + ci) * c.kk + kyx] : 0.0f;
+            const int ci = (int)(j / (ed * c.Cop)), rem = (int)(j - (int64_t)ci * ed * c.Cop);
+            const int e = rem / c.Cop, co = rem - e * c.Cop;
+            x = 0.0f;
+            if (co < c.Cout) {
+                const float *w = c.W + ((int64_t)co * c.Cin + ci) * c.kk;
+                if (c.ke > 0) {
+                    const int ey = e / c.ke, ex = e - ey * c.ke;
+                    for (int a = 0; a < 2; ++a)
+                        for (int b = 0; b < 2; ++b) {
+                            const int ky = a + c.k - 1 - ey, kx = b + c.k - 1 - ex;
+                            if (ky >= 0 && ky < c.k && kx >= 0 && kx < c.k) x = x + w[ky * c.k + kx];
+                        }
+                } else {
+                    x = w[e];
+                }
+                if (c.si >= 0) x = x / s;
+            }
             dst = c.wd; plane = nd;
         }
-        if (c.si >= 0) x = x / s;
         const S3Split q = s3_split(x);
         dst[j] = q.b0;
         dst[plane + j] = q.b1;
         dst[2 * plane + j] = q.b2;
     }
+}
+
+__global__ __launch_bounds__(256) void k_conv_prep(const ConvPrep *__restrict__ tab, const float *__restrict__ scale,
+                                                   double *loss_acc, int *step) {
+    if (loss_acc && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {   // a training step begins
+        *loss_acc = 0.0;
+        *step += 1;
+    }
+    const ConvPrep c = tab[blockIdx.y];
+    conv_prep_body(c, c.si >= 0 ? scale[c.si] : 1.0f, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                   (int64_t)gridDim.x * blockDim.x);
+}
+
+// one conv, no spectral norm (the standalone lrs_conv2d_* entry points)
+__global__ __launch_bounds__(256) void k_conv_prep1(ConvPrep c) {
+    conv_prep_body(c, 1.0f, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+}
+
+// Reflection-pad corrections of the effective-kernel data gradient of an upsampled, reflection-
+// padded 3 x 3 conv (pad 1).  The stride-2 4 x 4 conv over dL/dz treats the padded border as zeros;
+// the reference's ReflectionPad2d(1) also feeds padded row -1 from row 1 and row Hu from Hu - 2
+// (same for columns): extra (oy, ky) pairs (0, 0) -> source row 0 and (Hu - 1, 2) -> row Hs - 1,
+// and likewise (ox, kx) for the columns.  Four "lines": 0 / 1 = source rows 0 / Hs - 1 take every
+// term with a reflected row (any column, reflected or not); 2 / 3 = source columns 0 / Ws - 1 every
+// term with a reflected column and an unreflected row, so each term is counted once.  Three wide
+// launches (k_up_border_s, _mm, _add), scratch in the conv's col-gradient buffer:
+//   S[line][co][j][pos]  = the line's dL/dz summed over the positions that map to source pos via
+//                          tap j (j = kx for rows, ky for columns)
+//   corr[line][c][pos]   = sum_{co, j} W[co][c][tap(line, j)] S[line][co][j][pos]
+// then gx[c][perimeter pixel] += its row-line and column-line corrections.  w = the conv's fp32
+// weights (W / sigma) [Cout][Cin][3][3].
+constexpr int kUbC = 4, kUbCo = 32;
+
+__device__ __forceinline__ int ub_len(int line, int Hs, int Ws) { return line < 2 ? Ws : Hs; }
+
+__global__ __launch_bounds__(256) void k_up_border_s(const float *__restrict__ gz, int Cout, int Hs, int Ws, int Lmax,
+                                                     float *__restrict__ S) {
+    const int co = blockIdx.y, e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 4 * 3 * Lmax) return;
+    const int line = e / (3 * Lmax), j = (e / Lmax) % 3, pos = e % Lmax;
+    const int Hu = 2 * Hs, Wu = 2 * Ws, rows = line < 2, L = ub_len(line, Hs, Ws), Lu = rows ? Wu : Hu;
+    float v = 0.0f;
+    if (pos < L) {
+        const int ofix = (line & 1) == 0 ? 0 : (rows ? Hu - 1 : Wu - 1);
+        const float *g = gz + (int64_t)co * Hu * Wu;
+        for (int o = max(0, 2 * pos - 2); o <= min(Lu - 1, 2 * pos + 3); ++o) {
+            int u = o + j - 1;
+            if (rows) u = u < 0 ? -u : (u >= Lu ? 2 * (Lu - 1) - u : u);   // along x: reflected ends included
+            else if (u < 0 || u >= Lu) continue;                          // along y: unreflected rows only
+            if ((u >> 1) == pos) v += g[rows ? (int64_t)ofix * Wu + o : (int64_t)o * Wu + ofix];
+        }
+    }
+    S[(((int64_t)line * Cout + co) * 3 + j) * Lmax + pos] = v;
+}
+
+__global__ __launch_bounds__(256) void k_up_border_mm(const float *__restrict__ S, const float *__restrict__ w, int Cin,
+                                                      int Cout, int Hs, int Ws, int Lmax, float *__restrict__ corr) {
+    __shared__ float Ss[kUbCo * 3 * 128], Wl[kUbCo * kUbC * 3];
+    const int line = blockIdx.x, c0 = blockIdx.y * kUbC, p0 = blockIdx.z * 128;
+    const int rows = line < 2, L = ub_len(line, Hs, Ws), tfix = (line & 1) == 0 ? 0 : 2;
+    const int cl = threadIdx.x >> 7, pl = threadIdx.x & 127;   // 2 channels x 128 positions per pass
+    float acc[2] = {0.0f, 0.0f};
+    for (int co0 = 0; co0 < Cout; co0 += kUbCo) {
+        __syncthreads();
+        float sv[kUbCo * 3 * 128 / 256];   // all 48 loads issued before any LDS store (clamped, then masked)
+#pragma unroll
+        for (int u = 0; u < kUbCo * 3 * 128 / 256; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            const int col = e / 384, j = (e >> 7) % 3, pos = p0 + (e & 127), co = co0 + col;
+            const int cc = min(co, Cout - 1), pp = min(pos, Lmax - 1);
+            sv[u] = S[(((int64_t)line * Cout + cc) * 3 + j) * Lmax + pp];
+        }
+#pragma unroll
+        for (int u = 0; u < kUbCo * 3 * 128 / 256; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            const int col = e / 384, pos = p0 + (e & 127), co = co0 + col;
+            Ss[e] = (co < Cout && pos < L) ? sv[u] : 0.0f;
+        }
+        for (int e = threadIdx.x; e < kUbCo * kUbC * 3; e += blockDim.x) {
+            const int col = e / (kUbC * 3), c = c0 + (e / 3) % kUbC, j = e % 3, co = co0 + col;
+            Wl[e] = (co < Cout && c < Cin) ? w[((int64_t)co * Cin + c) * 9 + (rows ? tfix * 3 + j : j * 3 + tfix)] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = 2 * h + cl;
+            float a = acc[h];
+            for (int col = 0; col < kUbCo; ++col)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) a = __fmaf_rn(Wl[(col * kUbC + c) * 3 + j], Ss[(col * 3 + j) * 128 + pl], a);
+            acc[h] = a;
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int c = c0 + 2 * h + cl, pos = p0 + pl;
+        if (c < Cin && pos < L) corr[((int64_t)line * Cin + c) * Lmax + pos] = acc[h];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_up_border_add(const float *__restrict__ corr, int Cin, int Hs, int Ws,
+                                                       int Lmax, float *__restrict__ gx) {
+    const int nper = 2 * Ws + 2 * (Hs - 2);
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+    if (idx >= nper) return;
+    int sy, sx;
+    if (idx < Ws) { sy = 0; sx = idx; }
+    else if (idx < 2 * Ws) { sy = Hs - 1; sx = idx - Ws; }
+    else { const int r = idx - 2 * Ws; sy = 1 + (r >> 1); sx = (r & 1) ? Ws - 1 : 0; }
+    float v = 0.0f;
+    if (sy == 0) v += corr[((int64_t)0 * Cin + c) * Lmax + sx];
+    if (sy == Hs - 1) v += corr[((int64_t)1 * Cin + c) * Lmax + sx];
+    if (sx == 0) v += corr[((int64_t)2 * Cin + c) * Lmax + sy];
+    if (sx == Ws - 1) v += corr[((int64_t)3 * Cin + c) * Lmax + sy];
+    float *o = gx + ((int64_t)c * Hs + sy) * Ws + sx;
+    *o = *o + v;
 }
 
 // gx[c][sy][sx] (+)= sum over the x2 upsample children u of sum over the padded positions that

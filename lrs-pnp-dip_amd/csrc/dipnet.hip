@@ -152,6 +152,21 @@ int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *
 
 inline int r16(int x) { return (x + 15) & ~15; }
 
+// Data gradient of an upsampled stride-1 conv (the U-Net's up_1..up_4: nearest x2, then 2 x 2 unpadded
+// or reflection-padded 3 x 3) as a stride-2 conv over dL/dz with a (k+1) x (k+1) effective kernel on
+// the source grid (conv_bwd): 2.25x fewer products than correlating over the padded upsampled domain
+// and folding.  Returns k + 1, or 0 where the identity is not used.
+// Off by default: measured in the whole 196^2 training step (bench configs[2], 2 x 2 A/B runs) it is
+// ~1 % slower than the padded-domain correlation + fold -- the up_4 data-gradient work it saves ran
+// beside that layer's weight gradient anyway, and it adds a split-K reduce and the border launches
+// to the critical chain.  lrs_dip_set_upsample_dgrad(1) selects it (tests cover both).
+static int g_dip_upeff = 0;
+inline int up_eff_k(const ConvGeom &g) {
+    if (!g_dip_upeff || !g.up || g.stride != 1 || g.Hs < 2 || g.Ws < 2) return 0;
+    if (g.k == 3 && g.pad == 1) return 4;
+    if (g.k == 2 && g.pad == 0) return 3;
+    return 0;
+}
 int64_t conv_part_floats(const ConvGeom &g, int Cout) {
     const int P = g.Ho * g.Wo, kk = g.k * g.k, Kc = g.Cin * kk;
     int64_t m = gemm_part_floats(Cout, P, Kc);                       // forward
@@ -163,6 +178,7 @@ int64_t conv_part_floats(const ConvGeom &g, int Cout) {
     m = std::max(m, std::max(s3_part_floats(Cout, P, kk * r16(g.Cin)), s3_part_floats(Cout, Kc, P)));
     const int Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad);
     m = std::max(m, s3_part_floats(g.Cin, Qp, kk * r16(Cout)));
+    if (const int ke = up_eff_k(g)) m = std::max(m, s3_part_floats(g.Cin, g.Hs * g.Ws, ke * ke * r16(Cout)));
     return m;
 }
 
@@ -170,7 +186,8 @@ int64_t conv_part_floats(const ConvGeom &g, int Cout) {
 // the data-gradient operand WD [3][Cin][kk*Cop]
 inline int64_t wprep_fwd_elems(const ConvGeom &g, int Cout) { return 3 * (int64_t)Cout * g.k * g.k * r16(g.Cin); }
 inline int64_t wprep_elems(const ConvGeom &g, int Cout) {
-    return wprep_fwd_elems(g, Cout) + 3 * (int64_t)g.Cin * g.k * g.k * r16(Cout);
+    const int ke = up_eff_k(g);
+    return wprep_fwd_elems(g, Cout) + 3 * (int64_t)g.Cin * (ke ? ke * ke : g.k * g.k) * r16(Cout);
 }
 
 // Implicit-GEMM conv product on the split-bf16 kernel, with the same split-K / reduce tail as
@@ -214,8 +231,8 @@ inline int64_t implicit_min_pixels() {
 void wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, hipStream_t st) {
     const int kk = g.k * g.k;
     const int64_t n = wprep_elems(g, Cout) / 3;
-    hipLaunchKernelGGL(k_wprep, dim3(ew_blocks(n, 2048)), dim3(256), 0, st, w, Cout, g.Cin, kk, r16(g.Cin), r16(Cout),
-                       wf, wd);
+    const ConvPrep c{w, nullptr, wf, wd, Cout, g.Cin, kk, r16(g.Cin), r16(Cout), -1, g.k, wd ? up_eff_k(g) : 0};
+    hipLaunchKernelGGL(k_conv_prep1, dim3(ew_blocks(n, 2048)), dim3(256), 0, st, c);
 }
 
 // Pointwise conv product on k_pw (A: pre-split planes [3][M][lda], B: [K][N] fp32).
@@ -298,6 +315,36 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         return pw_launch(wpre + wprep_fwd_elems(g, Cout), (int64_t)g.Cin * r16(Cout), r16(Cout), g.Cin, gz, Cout, P,
                          gx, nullptr, accum_gx, st);
     if (plain_unit(g)) return gemm(1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st, accum_gx);
+    const int ke = up_eff_k(g);
+    const bool refl_border = g.pad_mode == LRS_PAD_REFLECT && g.k == 3;
+    const int Lmax = std::max(g.Ws, g.Hs);
+    // the border scratch (S and corr) lives in the col-gradient buffer, unused on this path
+    const bool border_fits = dcol && (int64_t)4 * (3 * Cout + g.Cin) * Lmax <= (int64_t)g.Cin * g.k * g.k * P;
+    if (implicit && wpre && ke && !accum_gx && (!refl_border || border_fits)) {
+        // gx = the stride-2 (ke x ke, zero pad 1) conv of dL/dz with the effective weights WE
+        // (k_conv_prep), then the reflection terms of the border rows / columns
+        const int Cop = r16(Cout), ke2 = ke * ke;
+        ConvGeom ge{};
+        ge.Cin = Cout; ge.Hs = g.Ho; ge.Ws = g.Wo; ge.up = 0; ge.Hu = g.Ho; ge.Wu = g.Wo;
+        ge.pad = 1; ge.pad_mode = LRS_PAD_ZERO; ge.k = ke; ge.stride = 2; ge.Ho = g.Hs; ge.Wo = g.Ws;
+        if ((g.Ho + 2 - ke) / 2 + 1 != g.Hs || (g.Wo + 2 - ke) / 2 + 1 != g.Ws) return LRS_E_INVALID;
+        rc = gemm_s3_conv(LdPre{wpre + wprep_fwd_elems(g, Cout), (int64_t)g.Cin * ke2 * Cop, ke2 * Cop, g.Cin},
+                          LdFwdTM{gz, Cout * P * 4, ge, Cop, nullptr}, gx, nullptr, nullptr, g.Cin, g.Hs * g.Ws,
+                          ke2 * Cop, part, part_cap, st);
+        if (rc) return rc;
+        if (refl_border) {
+            float *S = dcol, *corr = dcol + (int64_t)4 * 3 * Cout * Lmax;
+            hipLaunchKernelGGL(k_up_border_s, dim3((unsigned)((12 * Lmax + 255) / 256), (unsigned)Cout), dim3(256), 0, st,
+                               gz, Cout, g.Hs, g.Ws, Lmax, S);
+            hipLaunchKernelGGL(k_up_border_mm, dim3(4, (unsigned)((g.Cin + kUbC - 1) / kUbC), (unsigned)((Lmax + 127) / 128)),
+                               dim3(256), 0, st, S, w, g.Cin, Cout, g.Hs, g.Ws, Lmax, corr);
+            const int nper = 2 * g.Ws + 2 * (g.Hs - 2);
+            hipLaunchKernelGGL(k_up_border_add, dim3((unsigned)((nper + 255) / 256), (unsigned)g.Cin), dim3(256), 0, st,
+                               corr, g.Cin, g.Hs, g.Ws, Lmax, gx);
+        }
+        LRS_CHECK_LAUNCH();
+        return LRS_OK;
+    }
     if (!dcol) return LRS_E_WORKSPACE;
     const int Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad);
     if (implicit && wpre && g.stride == 1 && (int64_t)g.Cin * Qp <= (int64_t)Kc * P) {
@@ -1145,7 +1192,7 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
         __bf16 *wf = N.wpre_off >= 0 ? (__bf16 *)net->f(N.wpre_off) : nullptr;
         __bf16 *wd = (wf && N.d.in0 > 0) ? wf + wprep_fwd_elems(N.g, N.C) : nullptr;
         prep.push_back(ConvPrep{params + N.w_off, N.sn_index >= 0 ? net->f(N.wn_off) : nullptr, wf, wd, N.C, N.g.Cin,
-                                N.g.k * N.g.k, r16(N.g.Cin), r16(N.C), N.sn_index});
+                                N.g.k * N.g.k, r16(N.g.Cin), r16(N.C), N.sn_index, N.g.k, wd ? up_eff_k(N.g) : 0});
     }
     hipError_t e = hipSuccess;
     if (!tab.empty()) e = hipMemcpy(net->table(), tab.data(), sizeof(SnConv) * tab.size(), hipMemcpyHostToDevice);
@@ -1300,3 +1347,9 @@ extern "C" int lrs_dip_set_precision(int precision) {
 }
 
 extern "C" int lrs_dip_get_precision(void) { return g_dip_gemm_precision; }
+
+extern "C" int lrs_dip_set_upsample_dgrad(int mode) {
+    if (mode != 0 && mode != 1) return LRS_E_INVALID;
+    g_dip_upeff = mode;
+    return LRS_OK;
+}

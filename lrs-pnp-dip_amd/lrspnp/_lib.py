@@ -106,6 +106,7 @@ def _declare(L):
         "lrs_dipnet_reset_optimizer": (i32, [vp, vp]),
         "lrs_dipnet_forward": (i32, [vp, vp, vp]),
         "lrs_dipnet_backward": (i32, [vp, vp, vp, vp]),
+        "lrs_dip_set_upsample_dgrad": (i32, [i32]),
         "lrs_dipnet_set_ln_lambda": (i32, [vp, f32]),
         "lrs_dipnet_output": (c.c_size_t, [vp]),
         "lrs_dipnet_grads": (c.c_size_t, [vp]),

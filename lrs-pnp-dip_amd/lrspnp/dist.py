@@ -160,3 +160,80 @@ def gather_rows(X: torch.Tensor, ctx: Ctx):
     out = [None] * ctx.world
     dist.all_gather_object(out, x)
     return np.concatenate(out, axis=0) if ctx.rank == 0 else None
+
+
+# ---- one cube, task-parallel DIP ("DIP on GPU 0, sparse coding sharded over the rest") --
+#
+# In the DIP mains the two proxes of an outer iteration read the same iterate (sparse coding: X +
+# lambda_1 / mu_1, …1-LiP.py:362-392; DIP: X + lambda_2 / mu_2, :399-411), so they are independent:
+# rank 0 trains the DIP (batch 1, not data-parallel), ranks 1..W-1 code contiguous block ranges.
+# Every rank keeps the whole (replicated) cube state; per outer iteration rank 0 broadcasts U
+# (P x B floats) and the workers' Phi rows are all-gathered (nb x n_pad floats), after which every
+# rank applies the same deterministic ADMM update.  With one rank it is the ordinary step.
+
+
+class DipTaskSplit:
+    def __init__(self, Y, M, D, cfg, ctx: Ctx, image_shape, device="cuda"):
+        from .solver import LrsPnP
+        if cfg.lowrank != "dip":
+            raise ValueError("DipTaskSplit needs a DIP configuration (LrsPnPConfig.dip_1lip / dip_pro)")
+        self.ctx = ctx
+        self.s = LrsPnP(Y, M, D, cfg, device=device, image_shape=image_shape)
+        nb, W = self.s.nb, ctx.world
+        self.ranges = [(0, 0)] * W
+        if W > 1:
+            base, extra = divmod(nb, W - 1)
+            b = 0
+            for r in range(1, W):
+                c = base + (1 if r - 1 < extra else 0)
+                self.ranges[r] = (b, b + c)
+                b += c
+        self.maxc = max(b1 - b0 for b0, b1 in self.ranges) if W > 1 else nb
+        self.buf = None
+
+    def _exchange(self, stream):
+        s, ctx = self.s, self.ctx
+        nccl = dist.get_backend() == "nccl"
+        if nccl:
+            with torch.cuda.stream(stream):
+                dist.broadcast(s.U, src=0)
+        else:
+            stream.synchronize()
+            h = s.U.cpu()
+            dist.broadcast(h, src=0)
+            s.U.copy_(h)
+        n_pad = s.phi.shape[1]
+        b0, b1 = self.ranges[ctx.rank]
+        mine = torch.zeros((self.maxc, n_pad), dtype=torch.float32, device=s.phi.device)
+        if b1 > b0:
+            mine[: b1 - b0].copy_(s.phi[b0:b1])
+        if nccl:
+            if self.buf is None:
+                self.buf = torch.empty((ctx.world * self.maxc, n_pad), dtype=torch.float32, device=s.phi.device)
+            with torch.cuda.stream(stream):
+                dist.all_gather_into_tensor(self.buf, mine)
+            parts = self.buf.view(ctx.world, self.maxc, n_pad)
+        else:
+            stream.synchronize()
+            hs = [torch.empty((self.maxc, n_pad), dtype=torch.float32) for _ in range(ctx.world)]
+            dist.all_gather(hs, mine.cpu())
+            parts = hs
+        for r, (c0, c1) in enumerate(self.ranges):
+            if c1 > c0:
+                s.phi[c0:c1].copy_(parts[r][: c1 - c0], non_blocking=True)
+
+    def step(self):
+        s, ctx = self.s, self.ctx
+        main = torch.cuda.current_stream()
+        if ctx.world == 1:
+            return s.step()
+        if ctx.rank == 0:
+            lr = s.lowrank_stream
+            lr.wait_stream(main)
+            s.low_rank_dip(lr)
+            main.wait_stream(lr)
+        else:
+            b0, b1 = self.ranges[ctx.rank]
+            s.sparse_coding_range(b0, b1, stream=main)
+        self._exchange(main)
+        s.admm(main)

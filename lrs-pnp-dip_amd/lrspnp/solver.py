@@ -171,6 +171,22 @@ class LrsPnP:
         return ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox,
                         phi=self.phi, want_coefs=want_coefs, ws=self.ista_ws, stream=stream)
 
+    def sparse_coding_range(self, b0: int, b1: int, stream=None):
+        """Phi rows [b0, b1) only (the blocks of one task-parallel worker, lrspnp.dist.DipTaskSplit)."""
+        if b1 <= b0:
+            return
+        ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d[b0:b1], self.cols_d[b0:b1], self.n_pad,
+                   Yb=self.Yb[b0:b1], stream=stream)
+        ops.ista(self.Yb[b0:b1], self.obs[b0:b1], self.D, self.n, self.alpha[b0:b1], self.thr[b0:b1], self.cfg.Nit,
+                 self.prox, phi=self.phi[b0:b1], ws=self.ista_ws, stream=stream)
+
+    def admm(self, stream=None):
+        """col2im + closed-form X + dual updates from the current Phi and U (main_LRS_PnP.py:324-366)."""
+        ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
+                        self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms,
+                        stream=stream or torch.cuda.current_stream())
+        self.iteration += 1
+
     def low_rank(self, stream=None, s_out=None):
         warm = self.cfg.svt_warm and self.iteration > 0
         return ops.svt(self.X, self.L2, self.c2, self.tau, self.svt_ws, U=self.U, s_out=s_out, warm=warm,

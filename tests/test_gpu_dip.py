@@ -59,6 +59,10 @@ CONV_CASES = [
     (128, 198, 196, 196, 1, 1, 0, 1, 0),    # 196x196 last 1x1 (k_pw with col == NULL: 4 row blocks)
     (198, 128, 40, 41, 1, 1, 0, 1, 0),      # k_pw: K = 198 (planes padded to 208), N % 64 != 0
     (37, 250, 9, 13, 1, 1, 0, 1, 0),        # k_pw: ragged K, M = 250
+    (128, 128, 49, 49, 3, 1, 1, 1, 1),      # up_3 at 196x196: effective 4x4 stride-2 data gradient + reflection border
+    (64, 32, 10, 7, 3, 1, 1, 0, 1),         # upsampled zero-padded 3x3: effective kernel, no border terms
+    (128, 128, 25, 25, 2, 1, 0, 1, 1),      # up_2: effective 3x3 stride-2 data gradient
+    (24, 40, 2, 5, 3, 1, 1, 1, 1),          # reflection border on a 2-row source (corners only)
 ]
 
 
@@ -117,8 +121,15 @@ def test_conv_fwd_bwd(L, case, precision):
     assert rel(gx, xr.grad) < 2e-5
 
 
+@pytest.fixture(params=[0, 1], ids=["fold", "upeff"])
+def upsample_dgrad(L, request):
+    assert L.lrs_dip_set_upsample_dgrad(request.param) == 0
+    yield request.param
+    L.lrs_dip_set_upsample_dgrad(0)
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_implicit_fwd_bwd(L, case):
+def test_conv_implicit_fwd_bwd(L, case, upsample_dgrad):
     # col == NULL: the split-bf16 implicit-GEMM conv (im2col gathered in the kernel), and
     # lrs_conv2d_bwd_x_f32 (dW's col^T gathered from x); same tolerances as the explicit path
     cin, cout, H, W, k, stride, pad, pm, up = case
@@ -341,6 +352,39 @@ def test_unet_forward_and_first_step_vs_reference(L, golden):
         if u.bn:
             keep[offs[i][1]:offs[i][1] + u.cout] = False
     assert float((dp[keep] > 1e-4).float().mean()) < 1e-3
+
+
+def test_unet_gradients_implicit_sizes_vs_fp64(L, upsample_dgrad):
+    """Step-0 gradients of the U-Net at 52 x 52 (up_4 and the first convs on the implicit-GEMM
+    kernels, up_4's data gradient as the effective 4 x 4 stride-2 conv + reflection border terms)
+    against the fp64 restatement: 1e-4 (as at 36 x 36) or twice the fp32 torch error."""
+    from gen_dip_golden import flat_params
+    from lrspnp.dip import lipschitz_unet_units
+    units = lipschitz_unet_units(128, 128, 128)
+    H = 52
+    flat = torch.from_numpy(flat_params(units, 21, 128, H, H))
+    g = torch.Generator().manual_seed(5)
+    x, t = torch.rand(128, H, H, generator=g), torch.rand(128, H, H, generator=g)
+    m = (torch.rand(H * H, generator=g) > 0.1).float()
+    net = _engine(units, flat, H, H)
+    grads = {}
+    for dt in (torch.float64, torch.float32):
+        p = flat.to(dt).clone().requires_grad_(True)
+        dip_ref.loss_fn(dip_ref.forward(p, units, x.to(dt)), t.to(dt), m.to(dt)).backward()
+        grads[dt] = p.grad.double()
+    net.train_steps(x.cuda(), t.cuda(), m.cuda(), 1, use_graph=False)
+    torch.cuda.synchronize()
+    gd = net.grads.cpu()
+    offs, _ = dip_ref.param_offsets(units, 128, H, H)
+    # 1e-4, or twice the fp32-torch error where fp32 itself is further from fp64 (the first conv's
+    # weight gradient, at the end of the backward chain)
+    for i in range(len(units)):
+        Wg, bg, gg, beg = dip_ref.views(gd, units, i, offs, 128, H, H)
+        Wr, br, gr, ber = dip_ref.views(grads[torch.float64], units, i, offs, 128, H, H)
+        W32, b32, g32, be32 = dip_ref.views(grads[torch.float32], units, i, offs, 128, H, H)
+        assert rel(Wg, Wr) < max(1e-4, 2 * rel(W32, Wr)), (i, rel(Wg, Wr), rel(W32, Wr))
+        if gg is not None:
+            assert rel(gg, gr) < max(1e-4, 2 * rel(g32, gr)) and rel(beg, ber) < max(1e-4, 2 * rel(be32, ber)), i
 
 
 def test_unet_graph_replay_equals_eager(L):

@@ -231,3 +231,30 @@ def test_row_slab_sharding_matches_whole_cube(gpu, world, cube, bb):
     assert r["world"] == world
     assert r["rel_X"] < 1e-6 and r["rel_L1"] < 1e-6 and r["rel_L2"] < 1e-6, r
     assert np.allclose(r["conv_sharded"], r["conv_whole"], rtol=1e-6, atol=1e-9), r
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_task_parallel_dip_matches_one_rank(gpu, world):
+    """One cube, task-parallel DIP (lrspnp.dist.DipTaskSplit): rank 0 trains the
+    DIP, the other ranks code block ranges, U is broadcast and Phi all-gathered, every rank
+    applies the same update.  Against the one-rank solver on rank 0 (gloo, all ranks on cuda:0):
+    the kernels are deterministic, so the iterates agree to rounding (1e-6 relative L2) after 2
+    outer iterations of 5 DIP steps each."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(repo, "tools", "shard_check.py"),
+           "--backend", "gloo", "--cube", "36x36x40", "--bb", "12", "--steps", "2", "--dip", "5", "--nit", "10"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=repo)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r["world"] == world
+    assert r["rel_X"] < 1e-6 and r["rel_L1"] < 1e-6 and r["rel_L2"] < 1e-6 and r["rel_U"] < 1e-6, r

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--bb", type=int, default=8)
     ap.add_argument("--nit", type=int, default=20)
+    ap.add_argument("--dip", type=int, default=0, help="> 0: task-parallel DIP (DIP steps per outer iteration)")
     a = ap.parse_args()
     from lrspnp import LrsPnP, LrsPnPConfig
     from lrspnp import dist as D
@@ -38,6 +39,8 @@ def main():
     obs, clean, mask = synthetic_cube(H, W, B, seed=5)
     Y, M = unfold(obs), mask_matrix(mask, B)
     Dct = synthetic_dictionary(a.bb * a.bb, 256, 0)
+    if a.dip:
+        return dip_split(a, ctx, H, W, Y, M, Dct)
     cfg = LrsPnPConfig(bb=a.bb, sliding=a.bb, Nit=a.nit)
     s, (p0, p1) = D.slab_solver(Y, M, Dct, cfg, ctx)
     for _ in range(a.steps):
@@ -52,6 +55,30 @@ def main():
         out = {"world": ctx.world, "cube": a.cube, "steps": a.steps, "rel_X": rel(X, r.X), "rel_L1": rel(L1, r.L1),
                "rel_L2": rel(L2, r.L2), "conv_sharded": conv, "conv_whole": r.convergence(),
                "X_bitwise_equal": bool(np.array_equal(X, r.X.cpu().numpy()))}
+        print(json.dumps(out), flush=True)
+    if ctx.distributed:
+        torch.distributed.destroy_process_group()
+
+
+def dip_split(a, ctx, H, W, Y, M, Dct):
+    """Task-parallel DIP (lrspnp.dist.DipTaskSplit) vs the one-rank DIP solver on rank 0."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp import dist as D
+    from lrspnp.dip import DipConfig
+    cfg = LrsPnPConfig.dip_1lip(bb=a.bb, sliding=a.bb, Nit=a.nit, dip=DipConfig(num_iter=a.dip, early_stop=False))
+    t = D.DipTaskSplit(Y, M, Dct, cfg, ctx, image_shape=(H, W))
+    for _ in range(a.steps):
+        t.step()
+    torch.cuda.synchronize()
+    if ctx.rank == 0:
+        r = LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
+        for _ in range(a.steps):
+            r.step()
+        torch.cuda.synchronize()
+        rel = lambda u, v: float((u - v).norm() / max(float(v.norm()), 1e-30))
+        out = {"world": ctx.world, "cube": a.cube, "steps": a.steps, "dip_steps": a.dip, "rel_X": rel(t.s.X, r.X),
+               "rel_L1": rel(t.s.L1, r.L1), "rel_L2": rel(t.s.L2, r.L2), "rel_U": rel(t.s.U, r.U),
+               "X_bitwise_equal": bool(torch.equal(t.s.X, r.X)), "ranges": t.ranges}
         print(json.dumps(out), flush=True)
     if ctx.distributed:
         torch.distributed.destroy_process_group()
