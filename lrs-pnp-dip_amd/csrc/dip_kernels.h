@@ -733,6 +733,75 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd1(BnArgs a) {
     bn_apply_body(a, c, 0, 0.0 + s1, 0.0 + s2, redf, st_s);
 }
 
+// Split-K finish + BatchNorm(+act) of one channel in one launch (a channel fits one workgroup:
+// P <= 4 * kBn1Threads): z = sum of the GEMM's split-K partials (k_gemm_reduce's order) + bias,
+// stored for the backward, then k_bn_fwd1's statistics / normalisation / activation from the
+// values held in registers.  Replaces k_gemm_reduce + k_bn_fwd1 for the small-map convs.
+__global__ __launch_bounds__(kBn1Threads) void k_reduce_bn1(const float *__restrict__ part, int nsplit,
+                                                            const float *__restrict__ bias, BnArgs a) {
+    __shared__ double red[2 * kBn1Threads / 64];
+    __shared__ float redf[kBn1Threads / 64];
+    __shared__ float st_s[3];
+    const int c = blockIdx.y, t = threadIdx.x;
+    const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
+    float zv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = t + u * kBn1Threads;
+        zv[u] = 0.0f;
+        if (i >= a.P) continue;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int zz = 0;
+        for (; zz + 8 <= nsplit; zz += 8)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] += part[(int64_t)(zz + q) * MN + off + i];
+        for (; zz < nsplit; ++zz) acc[zz & 7] += part[(int64_t)zz * MN + off + i];
+        float v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+        if (bias) v = v + bias[c];
+        zv[u] = v;
+        const_cast<float *>(a.z)[off + i] = v;
+    }
+    if (t == 0) st_s[2] = zv[0];
+    __syncthreads();
+    const double K = (double)st_s[2];
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (t + u * kBn1Threads < a.P) {
+            const double d = (double)zv[u] - K;
+            s1 += d;
+            s2 += d * d;
+        }
+    int par = 0;
+    s1 = block_sum_d1(s1, red, par);
+    s2 = block_sum_d1(s2, red, par);
+    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    if (t == 0) {
+        const double m = s1 / a.P;
+        double var = s2 / a.P - m * m;
+        if (var < 0.0) var = 0.0;
+        const float m32 = (float)(K + m);
+        const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
+        st_s[0] = m32;
+        st_s[1] = is32;
+        a.mean[c] = m32;
+        a.invstd[c] = is32;
+        if (a.run_mean) {
+            const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
+            a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
+            a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+        }
+    }
+    __syncthreads();
+    const float m32 = st_s[0], is32 = st_s[1];
+    const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = t + u * kBn1Threads;
+        if (i < a.P) a.y[off + i] = act_fwd((zv[u] - m32) * is32 * gm + bt, a.act);
+    }
+}
+
 struct BnBwdArgs {
     const float *gy;             // [C][P] dL/dy
     const float *y, *z;          // activation output, conv output

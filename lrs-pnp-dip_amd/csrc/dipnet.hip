@@ -105,9 +105,10 @@ int64_t gemm_part_floats(int M, int N, int K) {
 
 // C = op(A) op(B) (+ bias) (/ *div); part: split-K scratch (>= gemm_part_floats)
 int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *bias, const float *div, int M,
-         int N, int K, float *part, int64_t part_cap, hipStream_t st, int accum = 0) {
+         int N, int K, float *part, int64_t part_cap, hipStream_t st, int accum = 0, int *nsplit_out = nullptr) {
     if (M <= 0 || N <= 0) return LRS_OK;
     const Split s = choose_split(M, N, K);
+    if (nsplit_out) *nsplit_out = s.S;   // > 1: the caller finishes the split-K sum (no reduce here)
     GemmArgs g{A, B, C, bias, div, M, N, K, s.kchunk, accum};
     if (s.S > 1) {
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
@@ -141,7 +142,7 @@ int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *
         else if (TA && !TB) hipLaunchKernelGGL((k_gemm64<1, 0>), grid, dim3(kGemmThreads), 0, st, g);
         else hipLaunchKernelGGL((k_gemm64<1, 1>), grid, dim3(kGemmThreads), 0, st, g);
     }
-    if (s.S > 1) {
+    if (s.S > 1 && !nsplit_out) {
         const int64_t MN = (int64_t)M * N;
         hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M,
                            N, bias, div, accum, C);
@@ -194,9 +195,10 @@ inline int64_t wprep_elems(const ConvGeom &g, int Cout) {
 // gemm().
 template <class LA, class LB>
 int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const float *div, int M, int N, int K,
-                 float *part, int64_t part_cap, hipStream_t st) {
+                 float *part, int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr) {
     if (M <= 0 || N <= 0) return LRS_OK;
     const Split s = choose_split(M, N, K, LRS_DIP_SPLIT_BF16, true);
+    if (nsplit_out) *nsplit_out = s.S;
     GemmArgs g{nullptr, nullptr, C, bias, div, M, N, K, s.kchunk, 0};
     if (s.S > 1) {
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
@@ -204,7 +206,7 @@ int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const 
     }
     dim3 grid((N + 127) / 128, (M + 127) / 128, s.S);
     hipLaunchKernelGGL((k_gemm_s3<LA, LB>), grid, dim3(kGemmThreads), 0, st, g, la, lb);
-    if (s.S > 1) {
+    if (s.S > 1 && !nsplit_out) {
         const int64_t MN = (int64_t)M * N;
         hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M, N,
                            bias, div, 0, C);
@@ -271,8 +273,9 @@ inline bool pw_ok(const ConvGeom &g, int Cout) { return plain_unit(g) && Cout <=
 // y = conv(x) + bias.  Explicit (col != NULL): im2col + GEMM.  Implicit (col == NULL, wpre =
 // the weight planes from wprep): tap-major implicit GEMM.
 int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bias, int Cout, float *col, float *y,
-             float *part, int64_t part_cap, hipStream_t st, const __bf16 *wpre = nullptr) {
+             float *part, int64_t part_cap, hipStream_t st, const __bf16 *wpre = nullptr, int *nsplit_out = nullptr) {
     const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
+    if (nsplit_out) *nsplit_out = 1;
     const float *B = x;
     if (plain_unit(g) && wpre)      // 1x1: pointwise kernel on the pre-split weights
         return pw_launch(wpre, (int64_t)Cout * r16(g.Cin), r16(g.Cin), Cout, x, g.Cin, P, y, bias, 0, st);
@@ -281,14 +284,14 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
         const int kk = g.k * g.k, Cp = r16(g.Cin);
         return gemm_s3_conv(LdPre{wpre, (int64_t)Cout * kk * Cp, kk * Cp, Cout},
                             LdFwdTM{x, g.Cin * g.Hs * g.Ws * 4, g, Cp, nullptr}, y, bias, nullptr, Cout, P, kk * Cp,
-                            part, part_cap, st);
+                            part, part_cap, st, nsplit_out);
     }
     if (!plain_unit(g)) {
         const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min(Kc, 65535));
         hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, st, x, g, col);
         B = col;
     }
-    return gemm(0, 0, w, B, y, bias, nullptr, Cout, P, Kc, part, part_cap, st);
+    return gemm(0, 0, w, B, y, bias, nullptr, Cout, P, Kc, part, part_cap, st, 0, nsplit_out);
 }
 
 // gw = gz col^T / div ; gx = col2im(w^T gz) (gw, gx nullable).  dcol: Kc*P floats when !plain.
@@ -816,13 +819,26 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
             float *z = bn ? net->f(N.z_off) : out;
             const float *w = N.sn_index >= 0 ? net->f(N.wn_off) : net->params + N.w_off;
             __bf16 *wp = N.wpre_off >= 0 ? (__bf16 *)net->f(N.wpre_off) : nullptr;
+            // a BN channel that fits one workgroup finishes the conv's split-K sum itself (k_reduce_bn1)
+            const bool fuse = bn && N.P <= 4 * kBn1Threads && bn_split(N.P) == 1;
+            int nsplit = 1;
             rc = conv_fwd(N.g, net->tensor(N.d.in0, x), w, net->params + N.b_off, N.C,
-                          N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st, wp);
+                          N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st, wp,
+                          fuse ? &nsplit : nullptr);
             if (rc) return rc;
-            rc = bn_fwd(z, out, bn ? net->params + N.gm_off : nullptr, bn ? net->params + N.bt_off : nullptr,
-                        net->f(N.mean_off), net->f(N.istd_off), bn ? net->bnstats + N.rs_off : nullptr,
-                        bn ? net->bnstats + N.rs_off + N.C : nullptr, N.C, N.P, N.d.act, 1e-5f, 0.1f, net->bnpart(), st,
-                        lip);
+            if (fuse && nsplit > 1) {
+                const BnArgs a{z, out, net->params + N.gm_off, net->params + N.bt_off, net->f(N.mean_off),
+                               net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C, nullptr, N.C,
+                               (int)N.P, 1, (int)N.P, 1, N.d.act, 1e-5f, 0.1f, lip, 0};
+                hipLaunchKernelGGL(k_reduce_bn1, dim3(1, N.C), dim3(kBn1Threads), 0, st, (const float *)net->f(net->part_off),
+                                   nsplit, (const float *)(net->params + N.b_off), a);
+                rc = LRS_OK;
+            } else {
+                rc = bn_fwd(z, out, bn ? net->params + N.gm_off : nullptr, bn ? net->params + N.bt_off : nullptr,
+                            net->f(N.mean_off), net->f(N.istd_off), bn ? net->bnstats + N.rs_off : nullptr,
+                            bn ? net->bnstats + N.rs_off + N.C : nullptr, N.C, N.P, N.d.act, 1e-5f, 0.1f, net->bnpart(), st,
+                            lip);
+            }
         } else if (N.d.kind == LRS_NODE_BN) {
             rc = bn_fwd(net->tensor(N.d.in0, x), out, net->params + N.gm_off, net->params + N.bt_off,
                         net->f(N.mean_off), net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C,
