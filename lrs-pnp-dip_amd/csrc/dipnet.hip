@@ -105,9 +105,10 @@ int64_t gemm_part_floats(int M, int N, int K) {
 
 // C = op(A) op(B) (+ bias) (/ *div); part: split-K scratch (>= gemm_part_floats)
 int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *bias, const float *div, int M,
-         int N, int K, float *part, int64_t part_cap, hipStream_t st, int accum = 0, int *nsplit_out = nullptr) {
+         int N, int K, float *part, int64_t part_cap, hipStream_t st, int accum = 0, int *nsplit_out = nullptr,
+         bool force_big = false) {
     if (M <= 0 || N <= 0) return LRS_OK;
-    const Split s = choose_split(M, N, K);
+    const Split s = choose_split(M, N, K, g_dip_gemm_precision, force_big);
     if (nsplit_out) *nsplit_out = s.S;   // > 1: the caller finishes the split-K sum (no reduce here)
     GemmArgs g{A, B, C, bias, div, M, N, K, s.kchunk, accum};
     if (s.S > 1) {
@@ -311,7 +312,11 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         rc = gemm_s3_conv(LdDense<true>{gz, P, Cout}, LdWgradTM{col, g.Cin * g.Hs * g.Ws * 4, g, nullptr, 0, 0}, gw,
                           nullptr, div, Cout, Kc, P, part, part_cap, st);
     } else {
-        rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st);
+        // a 1x1 conv's weight gradient (K = all pixels): 128-tiles with deep split-K on the split-bf16
+        // kernel (A/B in the 196^2 training step, configs[2]: 5.50 -> 5.65 outer it/s against the f32
+        // 64-tile kernel; alone the two are within 12 %, but the f32 kernel's 512 workgroups hold the
+        // CUs the concurrent data-gradient chain needs for longer)
+        rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st, 0, nullptr, plain_unit(g));
     }
     if (rc || !gx) return rc;
     if (plain_unit(g) && wpre)      // 1x1 data gradient: W^T planes (wprep's WD)
