@@ -341,7 +341,10 @@ constexpr int kS3TabInts = 16 * 128;  // k <= 4 (the 4 x 4 effective kernel of a
 
 template <class LA, class LB>
 __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
-    __shared__ __attribute__((aligned(16))) S3Tile As, Bs;
+    // one object: the epilogue reuses both operand images as a 4 x 32 x 68-float staging area
+    __shared__ __attribute__((aligned(16))) struct { S3Tile a, b; } ab;
+    static_assert(sizeof(ab) >= 4 * 32 * 68 * sizeof(float), "epilogue staging fits the operand images");
+    S3Tile &As = ab.a, &Bs = ab.b;
     __shared__ __attribute__((aligned(16))) int tab[kS3TabInts];
     // XCD-aware tile order: the hardware deals workgroup L to XCD L % 8 (placement matters for
     // speed only), so consecutive logical tiles -- neighbouring pixel tiles that share input rows,
@@ -371,26 +374,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
     float va[16], vb[16];
     RegP pa;   // LA::pre: the weight planes
     static_assert(!LB::pre, "B is never pre-split");
-    if constexpr (LA::pre) la.load(m0, kbeg, kend, pa);
-    else la.load(m0, kbeg, kend, va);
-    if constexpr (PREP) lb.load(n0, kbeg, kend, vb, 0);
-    else lb.load(n0, kbeg, kend, vb);
-    int tb = 0;
-    for (int k0 = kbeg; k0 < kend; k0 += kS3K) {
-        if constexpr (LA::pre) s3_store_pre(As, pa);
-        else s3_store<LA::kc>(As, va);
-        s3_store<LB::kc>(Bs, vb);
-        if constexpr (PREP) {
-            if (k0 + kS3K < kend) lb.prepare(k0 + kS3K, kend, tb ^ 1);
-        }
-        __syncthreads();
-        if (k0 + kS3K < kend) {
-            if constexpr (LA::pre) la.load(m0, k0 + kS3K, kend, pa);
-            else la.load(m0, k0 + kS3K, kend, va);
-            if constexpr (PREP) lb.load(n0, k0 + kS3K, kend, vb, tb ^ 1);
-            else lb.load(n0, k0 + kS3K, kend, vb);
-        }
-        tb ^= 1;
+    auto mma = [&]() {
         s3bf8 fb[4][3];
 #pragma unroll
         for (int b = 0; b < 4; ++b) s3_frag(Bs, wn + 16 * b + jl, gk, fb[b]);
@@ -401,30 +385,108 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
 #pragma unroll
             for (int b = 0; b < 4; ++b) acc[a][b] = s3_mfma6(fa, fb[b], acc[a][b]);
         }
-        __syncthreads();
+    };
+    if constexpr (PREP) {
+        if constexpr (LA::pre) la.load(m0, kbeg, kend, pa);
+        else la.load(m0, kbeg, kend, va);
+        lb.load(n0, kbeg, kend, vb, 0);
+        int tb = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += kS3K) {
+            if constexpr (LA::pre) s3_store_pre(As, pa);
+            else s3_store<LA::kc>(As, va);
+            s3_store<LB::kc>(Bs, vb);
+            if (k0 + kS3K < kend) lb.prepare(k0 + kS3K, kend, tb ^ 1);
+            __syncthreads();
+            if (k0 + kS3K < kend) {
+                if constexpr (LA::pre) la.load(m0, k0 + kS3K, kend, pa);
+                else la.load(m0, k0 + kS3K, kend, va);
+                lb.load(n0, k0 + kS3K, kend, vb, tb ^ 1);
+            }
+            tb ^= 1;
+            mma();
+            __syncthreads();
+        }
+    } else {
+        if constexpr (LA::pre) la.load(m0, kbeg, kend, pa);
+        else la.load(m0, kbeg, kend, va);
+        lb.load(n0, kbeg, kend, vb);
+        for (int k0 = kbeg; k0 < kend; k0 += kS3K) {
+            if constexpr (LA::pre) s3_store_pre(As, pa);
+            else s3_store<LA::kc>(As, va);
+            s3_store<LB::kc>(Bs, vb);
+            __syncthreads();
+            if (k0 + kS3K < kend) {
+                if constexpr (LA::pre) la.load(m0, k0 + kS3K, kend, pa);
+                else la.load(m0, k0 + kS3K, kend, va);
+                lb.load(n0, k0 + kS3K, kend, vb);
+            }
+            mma();
+            __syncthreads();
+        }
     }
     float *C = g.C + (int64_t)bz * g.M * g.N;
     const bool final_out = gridDim.z == 1;
     const float dv = (final_out && g.div) ? *g.div : 1.0f;
+    if ((g.N & 3) != 0 || (reinterpret_cast<uintptr_t>(g.C) & 15) != 0) {
+        // rows not float4-aligned (odd pixel counts): straight from the MFMA layout, 64-B runs
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int n = n0 + wn + 16 * b + jl;
+            for (int b = 0; b < 4; ++b) {
+                const int n = n0 + wn + 16 * b + jl;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wm + 16 * a + 4 * gk + r;
-                if (m < g.M && n < g.N) {
-                    float v = acc[a][b][r];
-                    if (final_out) {
-                        if (g.bias) v = v + g.bias[m];
-                        if (g.div) v = v / dv;
-                        if (g.accum) v = C[(int64_t)m * g.N + n] + v;
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + wm + 16 * a + 4 * gk + r;
+                    if (m < g.M && n < g.N) {
+                        float v = acc[a][b][r];
+                        if (final_out) {
+                            if (g.bias) v = v + g.bias[m];
+                            if (g.div) v = v / dv;
+                            if (g.accum) v = C[(int64_t)m * g.N + n] + v;
+                        }
+                        C[(int64_t)m * g.N + n] = v;
                     }
-                    C[(int64_t)m * g.N + n] = v;
                 }
             }
+        return;
+    }
+    // float4-aligned rows: through LDS (the operand images are dead after the last barrier).
+    // Each wave writes half of its 64 x 64 sub-tile at a time as [row][col] (row stride 68
+    // floats) and reads it back as float4 runs, so 16 lanes store 256 contiguous bytes of a row
+    float *E = reinterpret_cast<float *>(&ab) + wv * 32 * 68;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+        for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) E[(16 * a2 + 4 * gk + r) * 68 + 16 * b + jl] = acc[2 * hf + a2][b][r];
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's half-tile is in LDS (wave-local)
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int idx = lane + 64 * i, rr = idx >> 4, q = 4 * (idx & 15);
+            const int m = m0 + wm + 32 * hf + rr, n = n0 + wn + q;
+            if (m < g.M && n < g.N) {   // N % 4 == 0: a float4 run is all in or all out
+                float4 v = *reinterpret_cast<const float4 *>(E + rr * 68 + q);
+                float4 *c = reinterpret_cast<float4 *>(C + (int64_t)m * g.N + n);
+                if (final_out) {
+                    if (g.bias) {
+                        const float bs = g.bias[m];
+                        v.x = v.x + bs; v.y = v.y + bs; v.z = v.z + bs; v.w = v.w + bs;
+                    }
+                    if (g.div) { v.x = v.x / dv; v.y = v.y / dv; v.z = v.z / dv; v.w = v.w / dv; }
+                    if (g.accum) {
+                        const float4 o = *c;
+                        v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
+                    }
+                }
+                *c = v;
+            }
         }
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // ---- pointwise (1x1, stride 1, unpadded) conv product -----------------------------------------

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblrspnp_hip.so")
+# LRSPNP_LIB: another build of the same library (A/B timing of kernel variants, tools/ab_*.sh)
+LIB_PATH = os.environ.get("LRSPNP_LIB") or os.path.join(_HERE, "liblrspnp_hip.so")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 LRS_OK = 0

@@ -1,0 +1,39 @@
+"""Median DIP training-step time (ms) of the bench's network (configs[2]: my_Lipschitz_Unet
+198->128->198 on 196x196), for A/B of kernel builds (LRSPNP_LIB).  Several timed rounds of
+`--steps` steps; prints each round and the median.
+
+    python tools/dip_steptime.py [--hw 196] [--bands 198] [--steps 100] [--rounds 7] [--graph]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lrs-pnp-dip_amd"))
+import torch  # noqa: E402
+from lrspnp.dip import DipNet, lipschitz_unet_nodes  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--hw", type=int, default=196)
+ap.add_argument("--bands", type=int, default=198)
+ap.add_argument("--steps", type=int, default=100)
+ap.add_argument("--rounds", type=int, default=7)
+ap.add_argument("--graph", action="store_true")
+a = ap.parse_args()
+net = DipNet(lipschitz_unet_nodes(a.bands, a.bands, 128), a.bands, a.hw, a.hw)
+net.init_params(0)
+g = torch.Generator(device="cuda").manual_seed(0)
+x = torch.rand(a.bands, a.hw, a.hw, device="cuda", generator=g)
+t = torch.rand(a.bands, a.hw, a.hw, device="cuda", generator=g)
+m = (torch.rand(a.hw, a.hw, device="cuda", generator=g) > 0.2).float()
+net.train_steps(x, t, m, 10, use_graph=a.graph)
+torch.cuda.synchronize()
+res = []
+for r in range(a.rounds):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    net.train_steps(x, t, m, a.steps, use_graph=a.graph)
+    e1.record()
+    torch.cuda.synchronize()
+    res.append(e0.elapsed_time(e1) / a.steps)
+print("dip step ms:", " ".join(f"{v:.4f}" for v in res), "median", f"{statistics.median(res):.4f}")
