@@ -1074,11 +1074,11 @@ __global__ __launch_bounds__(256) void k_sn_gram_reduce(const SnConv *convs, dou
     if (PT.a[p] != PT.b[p]) G[j * kSnMaxDim + i] = v;
 }
 
-// number of eigenvalues of the symmetric tridiagonal (diag al, squared off-diagonal be2) above x:
-// k minus the sign changes of the characteristic-polynomial sequence p_i = (al_i - x) p_{i-1}
-// - be2_{i-1} p_{i-2} (division-free; rescaled by a power of two every 4 terms, which changes no
-// sign).  Four terms per block: their eight LDS reads are issued together, off the serial chain.
-// (Measured: holding al / be2 in registers and broadcasting with readlane is slower.)
+// number of eigenvalues of the symmetric tridiagonal T_n above x, T_n given as ab[i] = {alpha_i,
+// beta_{i-1}^2}: n minus the sign changes of the characteristic-polynomial sequence p_i =
+// (alpha_i - x) p_{i-1} - beta_{i-1}^2 p_{i-2} (division-free; rescaled by a power of two every 4
+// terms, which changes no sign).  The next four terms' LDS reads are in flight while four are
+// evaluated.
 __device__ __forceinline__ void sturm_term(double a, double b2, double x, double &p, double &pm, int &changes) {
     double pn = __fma_rn(a - x, p, -b2 * pm);
     // a zero takes the sign opposite to its predecessor: perturb it to -p * 2^-600 (the usual
@@ -1089,70 +1089,72 @@ __device__ __forceinline__ void sturm_term(double a, double b2, double x, double
     p = pn;
 }
 
-__device__ int sturm_gt(const double *al, const double *be2, int k, double x) {
-    double pm = 1.0, p = al[0] - x;
+__device__ int sturm_gt(const double2 *ab, int n, double x) {
+    double pm = 1.0, p = ab[0].x - x;
     p = p != 0.0 ? p : -0x1p-600;              // p_0 = 1 > 0: a zero p_1 counts as negative
     int changes = p < 0.0;
     int i = 1;
-    for (; i + 4 <= k; i += 4) {
-        const double a0 = al[i], a1 = al[i + 1], a2 = al[i + 2], a3 = al[i + 3];
-        const double b0 = be2[i - 1], b1 = be2[i], b2 = be2[i + 1], b3 = be2[i + 2];
-        sturm_term(a0, b0, x, p, pm, changes);
-        sturm_term(a1, b1, x, p, pm, changes);
-        sturm_term(a2, b2, x, p, pm, changes);
-        sturm_term(a3, b3, x, p, pm, changes);
+    double2 c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = ab[min(i + j, kSnMaxDim - 1)];
+    for (; i + 4 <= n; i += 4) {
+        double2 nx[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nx[j] = ab[min(i + 4 + j, kSnMaxDim - 1)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sturm_term(c[j].x, c[j].y, x, p, pm, changes);
         int e;
         frexp(fabs(p) > fabs(pm) ? p : pm, &e);
         p = ldexp(p, -e);
         pm = ldexp(pm, -e);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = nx[j];
     }
-    for (; i < k; ++i) sturm_term(al[i], be2[i - 1], x, p, pm, changes);
-    return k - changes;
+    for (; i < n; ++i) sturm_term(ab[i].x, ab[i].y, x, p, pm, changes);
+    return n - changes;
 }
 
-// Largest eigenvalue of the symmetric tridiagonal T_k (diag al, off-diagonal be, be2 = be^2):
-// the Gershgorin interval (or, with keep, the bracket already in lohi), then `rounds`
-// 256-point multisections (each narrows it 257x).  Whole block; result uniform.
-__device__ double tridiag_max_eig(const double *al, const double *be, const double *be2, int k, int rounds,
-                                  double *lohi, int *best, bool keep = false) {
+// One 256-point multisection round on T_n: thread t tests x_t = base + step (t + 1); returns (to
+// every thread) the largest t with an eigenvalue above x_t, or -1.  So the top eigenvalue lies in
+// (x_bt, x_{bt+1}] with x_{-1} = base, recomputed by the caller with sn_grid (the same rounding).
+// `best` holds 3 slots used round-robin: a round's slot was reset by thread 0 in the previous
+// round, before its barrier, and last read two rounds ago.  One barrier per round.
+__device__ __forceinline__ double sn_grid(double base, double step, int t) { return base + step * (double)(t + 1); }
+
+__device__ __forceinline__ int sn_round(const double2 *ab, int n, double base, double step, int *best, int &rnd) {
     const int t = threadIdx.x;
-    if (t == 0 && !keep) {
-        double lo = 1e300, hi = -1e300;
-        for (int i = 0; i < k; ++i) {
-            const double r = (i > 0 ? be[i - 1] : 0.0) + (i + 1 < k ? be[i] : 0.0);
-            lo = fmin(lo, al[i] - r);
-            hi = fmax(hi, al[i] + r);
-        }
-        lohi[0] = fmax(lo, 0.0);
-        lohi[1] = hi;
-    }
+    int *slot = best + rnd % 3;
+    if (t == 0) best[(rnd + 1) % 3] = -1;
+    if (sturm_gt(ab, n, sn_grid(base, step, t)) >= 1) atomicMax(slot, t);
     __syncthreads();
-    for (int round = 0; round < rounds; ++round) {
-        const double lo = lohi[0], hi = lohi[1];
-        if (!(hi - lo > 1e-15 * hi)) break;
-        const double x = lo + (hi - lo) * (double)(t + 1) / 257.0;
-        if (t == 0) *best = -1;
-        __syncthreads();
-        if (x > lo && x < hi && sturm_gt(al, be2, k, x) >= 1) atomicMax(best, t);
-        __syncthreads();
-        if (t == 0) {
-            const int bt = *best;
-            const double nlo = bt >= 0 ? lo + (hi - lo) * (double)(bt + 1) / 257.0 : lo;
-            const double nhi = bt + 1 <= 255 ? lo + (hi - lo) * (double)(bt + 2) / 257.0 : hi;
-            lohi[0] = nlo;
-            lohi[1] = fmax(nlo, nhi);
-        }
-        __syncthreads();
+    const int bt = *slot;
+    ++rnd;
+    return bt;
+}
+
+// Narrow [lo, hi] (top eigenvalue inside, lo exclusive) by 257x per round until hi - lo <= tol hi
+// (at most 12 rounds: 29 decades; tol >= 1e-12 stays far above the rounding of the grid).
+__device__ __forceinline__ void sn_multisect(const double2 *ab, int n, double &lo, double &hi, double tol, int *best,
+                                             int &rnd) {
+    for (int it = 0; it < 12 && hi - lo > tol * hi; ++it) {
+        const double step = (hi - lo) * (1.0 / 257.0);
+        const int bt = sn_round(ab, n, lo, step, best, rnd);
+        const double nlo = bt >= 0 ? sn_grid(lo, step, bt) : lo;
+        const double nhi = bt < 255 ? sn_grid(lo, step, bt + 1) : hi;
+        lo = nlo;
+        hi = fmax(nlo, nhi);
     }
-    return 0.5 * (lohi[0] + lohi[1]);
 }
 
 // One workgroup (256 threads) per conv: Lanczos (no reorthogonalisation: the extreme Ritz value
 // converges regardless, Paige) with the Gram in registers (thread t holds half a row, 64
-// doubles).  Every 8 steps from step 24 the largest Ritz value is located to ~1e-10 (4
-// multisection rounds); the iteration stops when it moved less than 1e-11 relative (typically
-// 30-40 steps for these weights instead of m = 128), then 2 more rounds from that check's bracket
-// (8 from Gershgorin if no check converged) pin lambda_max.
+// doubles).  The Gershgorin bounds of T_k are kept in registers as rows become final.
+// Convergence: at step 24 the top Ritz value is bracketed to a cell of width <= 5e-10 of it
+// (multisection from the Gershgorin interval); every 4 steps after that ONE round over the 256
+// cells of that width above the bracket's low end relocates it (the top Ritz value only grows
+// with k, Cauchy interlacing).  Converged when it stayed in its cell for 4 steps (typically 28-40
+// steps for these weights instead of m = 128); one more round then narrows the cell 257x.
+// A move of more than 256 cells re-brackets from the Gershgorin bound.
 // sigma32 = float(sqrt(lambda_max)); scale = max(1, sigma32 / ln_lambda) (float32, as torch).
 __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const double *gram, float *sigma,
                                                   float *scale, float ln_lambda, long long *prof) {
@@ -1162,10 +1164,10 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     const double *G = gram + (int64_t)blockIdx.x * kSnGramDoubles;
     extern __shared__ double Gs[];                // [kSnMaxDim][kSnMaxDim + 1] (dynamic, 129 KB)
     __shared__ __attribute__((aligned(16))) double q[kSnMaxDim];
-    __shared__ double al[kSnMaxDim], be[kSnMaxDim], be2[kSnMaxDim], lohi[2];
-    __shared__ int best_s;
+    __shared__ __attribute__((aligned(16))) double2 ab[kSnMaxDim];   // {alpha_i, beta_{i-1}^2}
+    __shared__ int best_s[3];
     const int t = threadIdx.x, row = t >> 1, half = t & 1;
-    // sum the split-K partials with coalesced loads into LDS, then each thread takes half a row
+    if (t < 3) best_s[t] = -1;
     // the reduced Gram (k_sn_gram_reduce): 16-B loads, all in flight
     {
         double2 pv[32];
@@ -1183,7 +1185,7 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
 #pragma unroll
     for (int c = 0; c < 64; ++c) g[c] = Gs[row * (kSnMaxDim + 1) + half * 64 + c];
     if (prof && t == 0) prof[blockIdx.x * 8 + 1] = wall_clock64();
-    int par = 0;
+    int par = 0, rnd = 0;
     // Lanczos on the unnormalised residual r_k (r_0 = start vector): one matvec u' = G r_k, one
     // two-value reduction (||r_k||^2, r_k.u'), then beta_k = ||r_k||, q_k = r_k / beta_k,
     // alpha_k = r_k.u' / beta_k^2 and r_{k+1} = u'/beta_k - alpha_k q_k - beta_k q_{k-1}.
@@ -1191,12 +1193,16 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     // (Measured: warm-starting from the previous step's top Ritz vector does not shorten the
     // iteration: with Adam at lr 0.1 the weights change by O(their size) every step.)
     double rr = (row < m) ? 1.0 + 0.5 * sin(0.7 * (double)row + 0.3) : 0.0;
-    double qprev = 0.0, theta_prev = -1.0;
+    double qprev = 0.0;
+    // uniform: Gershgorin max / min over the final rows of T, the last row's alpha and beta
+    double gmax = -1e300, gmin = 1e300, a_last = 0.0, b_last = 0.0;
+    double blo = 0.0, bhi = 0.0;                  // bracket of the last check's top Ritz value
+    bool have = false, converged = false;
     __shared__ double red2[2][8];
     if (half == 0) q[row] = rr;
     __syncthreads();
     int k = 0;
-    bool converged = false;
+    long long tcheck = 0, ccheck = 0;
     for (; k < m; ++k) {
         // all 32 b128 reads of this thread's half of q are issued before the first FMA (left to
         // itself the compiler waited on each read: ~2.5 us per step instead of ~0.5)
@@ -1225,32 +1231,76 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
         const double s_ru = (red2[1][4 * par] + red2[1][4 * par + 1]) + (red2[1][4 * par + 2] + red2[1][4 * par + 3]);
         par ^= 1;
         const double b = sqrt(s_rr);
-        if (k > 0 && !(b > 1e-14 * fabs(al[k - 1]))) break;   // invariant subspace: T_k is exact
+        if (k > 0 && !(b > 1e-14 * fabs(a_last))) break;   // invariant subspace: T_k is exact
         const double ib = 1.0 / b;
         const double a = s_ru * ib * ib;
-        if (t == 0) {
-            al[k] = a;
-            if (k > 0) { be[k - 1] = b; be2[k - 1] = s_rr; }
+        if (t == 0) ab[k] = make_double2(a, s_rr);
+        // row k-1 is final now (its off-diagonals beta_{k-1}, beta_k are known); row k so far
+        if (k > 0) {
+            const double r = b_last + b;
+            gmax = fmax(gmax, a_last + r);
+            gmin = fmin(gmin, a_last - r);
         }
+        a_last = a;
+        b_last = k > 0 ? b : 0.0;
         const double qk = rr * ib;
         rr = u * ib - a * qk - (k > 0 ? b : 0.0) * qprev;
         qprev = qk;
         if (k + 1 == m) { ++k; break; }
-        if (k + 1 >= 24 && ((k + 1) & 7) == 0) {
-            __syncthreads();
-            const double th = tridiag_max_eig(al, be, be2, k + 1, 4, lohi, &best_s);
-            const bool conv = fabs(th - theta_prev) <= 1e-11 * th;
-            theta_prev = th;
-            if (conv) { ++k; converged = true; break; }
+        if (k + 1 >= 24 && ((k + 1) & 3) == 0) {
+            __syncthreads();                      // ab[k] visible
+            const long long tc0 = prof ? wall_clock64() : 0, cc0 = prof ? clock64() : 0;
+            const int n = k + 1;
+            const double ghi = fmax(gmax, a_last + b_last);
+            double lo, hi = ghi;
+            bool need = true;
+            if (have) {
+                const double w = bhi - blo;
+                const int bt = sn_round(ab, n, blo, w, best_s, rnd);
+                if (bt < 0) {
+                    converged = true;              // still inside [blo, bhi]
+                    need = false;
+                } else if (bt < 255) {
+                    const double b0 = blo;
+                    blo = sn_grid(b0, w, bt);
+                    bhi = sn_grid(b0, w, bt + 1);
+                    need = false;
+                } else {
+                    lo = sn_grid(blo, w, 255);
+                }
+            } else {
+                lo = fmax(0.0, fmin(gmin, a_last - b_last));
+            }
+            if (need) {
+                sn_multisect(ab, n, lo, hi, 5e-10, best_s, rnd);
+                blo = lo;
+                bhi = hi;
+                have = true;
+            }
+            if (prof) { tcheck += wall_clock64() - tc0; ccheck += clock64() - cc0; }
+            if (converged) { ++k; break; }
         }
         if (half == 0) q[row] = rr;                   // the matvec reads of q finished before the barrier
         __syncthreads();
     }
     __syncthreads();
-    if (prof && t == 0) { prof[blockIdx.x * 8 + 2] = wall_clock64(); prof[blockIdx.x * 8 + 4] = k; }
-    // converged at a check: that check's bracket (4 rounds from Gershgorin, width <= ~1e-9 lmax,
-    // far below the float32 rounding of sigma) is the result; else 8 rounds from Gershgorin
-    const double lmax = m <= 0 ? 0.0 : converged ? 0.5 * (lohi[0] + lohi[1]) : tridiag_max_eig(al, be, be2, k, 8, lohi, &best_s);
+    if (prof && t == 0) { prof[blockIdx.x * 8 + 2] = wall_clock64(); prof[blockIdx.x * 8 + 4] = k; prof[blockIdx.x * 8 + 5] = tcheck; prof[blockIdx.x * 8 + 6] = ccheck; }
+    double lmax = 0.0;
+    if (m > 0) {
+        double lo, hi;
+        if (converged) {
+            // one more round inside the converged cell (width <= 5e-10 lmax -> <= 2e-12)
+            lo = blo;
+            hi = bhi;
+            sn_multisect(ab, k, lo, hi, 0.5 * (bhi - blo) / bhi, best_s, rnd);
+        } else {
+            // T_k exhausted (k = m) or exact (invariant subspace): from its Gershgorin interval
+            lo = fmax(0.0, fmin(gmin, a_last - b_last));
+            hi = fmax(gmax, a_last + b_last);
+            sn_multisect(ab, k, lo, hi, 1e-12, best_s, rnd);
+        }
+        lmax = 0.5 * (lo + hi);
+    }
     if (prof && t == 0) prof[blockIdx.x * 8 + 3] = wall_clock64();
     if (t == 0) {
         const float s32 = (float)sqrt(fmax(lmax, 0.0));
@@ -1314,20 +1364,23 @@ __global__ __launch_bounds__(256) void k_masked_mse(const float *__restrict__ ou
 }
 
 // Loss head of a training step whose last node is a conv without BN (both reference nets): the
-// masked MSE (as k_masked_mse: loss_acc += sum d^2, dL/dout = -(2/(C P)) d m) fused with that
-// node's activation backward dL/dz = act'(out) dL/dout and its bias gradient sum_p dL/dz: one pass
-// instead of masked-MSE + BN-backward statistics + BN-backward apply.  Bias partials [c][chunk]
-// (fp64) are summed in chunk order by the last workgroup of each channel to finish (a per-channel
-// counter, reset by that workgroup), so the bias gradient is deterministic.
+// masked MSE (as k_masked_mse: sum d^2, dL/dout = -(2/(C P)) d m) fused with that node's
+// activation backward dL/dz = act'(out) dL/dout and its bias gradient sum_p dL/dz: one pass
+// instead of masked-MSE + BN-backward statistics + BN-backward apply.  Grid (S, C), S ~ P / 4096
+// (a few thousand workgroups: the pass is HBM-bound only with many loads in flight).  Partials
+// (fp64) go to part[c][S] (bias) and part[C S + c][S] (loss); the last workgroup of a channel to
+// finish (per-channel counter) sums that channel's partials in order, the last channel to finish
+// (counter cnt[C]) sums the channel losses in order into loss_acc: bias gradient and loss are both
+// deterministic.  Counters are reset by their last arriver.
 __global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out, const float *__restrict__ target,
                                                   const float *__restrict__ mask, int C, int64_t P, int chunk,
                                                   int vec, int act, float *__restrict__ gz, double *loss_acc,
-                                                  double *__restrict__ bpart, int *__restrict__ cnt,
+                                                  double *__restrict__ part, int *__restrict__ cnt,
                                                   float *__restrict__ gbias) {
     __shared__ double red[8];
     __shared__ int last;
     const float norm = (float)(2.0 / ((double)C * (double)P));
-    const int c = blockIdx.y;
+    const int c = blockIdx.y, S = gridDim.x;
     const int64_t off = (int64_t)c * P;
     const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(P, i0 + chunk);
     double s = 0.0, sb = 0.0;
@@ -1335,20 +1388,30 @@ __global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out,
         const float4 *o4 = reinterpret_cast<const float4 *>(out + off), *t4 = reinterpret_cast<const float4 *>(target + off);
         const float4 *m4 = reinterpret_cast<const float4 *>(mask);
         float4 *g4 = reinterpret_cast<float4 *>(gz + off);
-        for (int64_t q = (i0 >> 2) + threadIdx.x; q < (i1 >> 2); q += blockDim.x) {
-            const float4 ov = o4[q], tv = t4[q];
-            const float4 mv = mask ? m4[q] : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-            const float oe[4] = {ov.x, ov.y, ov.z, ov.w}, te[4] = {tv.x, tv.y, tv.z, tv.w},
-                        me[4] = {mv.x, mv.y, mv.z, mv.w};
-            float ge[4];
+        const int q0 = (int)(i0 >> 2), q1 = (int)(i1 >> 2);
+        // two float4 per thread per trip: both loads of both in flight together
+        for (int q = q0 + threadIdx.x; q < q1; q += 2 * blockDim.x) {
+            const bool hb = q + (int)blockDim.x < q1;
+            const int qb = hb ? q + (int)blockDim.x : q;   // loads unconditional (all in flight together)
+            const float4 ov0 = o4[q], tv0 = t4[q], ov1 = o4[qb], tv1 = t4[qb];
+            const float4 one4 = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+            const float4 mv0 = mask ? m4[q] : one4, mv1 = mask ? m4[qb] : one4;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float d = te[e] * me[e] - oe[e] * me[e];
-                s += (double)d * (double)d;
-                ge[e] = act_bwd((-(norm * d)) * me[e], oe[e], act);
-                sb += (double)ge[e];
+            for (int h = 0; h < 2; ++h) {
+                if (h == 1 && !hb) break;
+                const float4 ov = h ? ov1 : ov0, tv = h ? tv1 : tv0, mv = h ? mv1 : mv0;
+                const float oe[4] = {ov.x, ov.y, ov.z, ov.w}, te[4] = {tv.x, tv.y, tv.z, tv.w},
+                            me[4] = {mv.x, mv.y, mv.z, mv.w};
+                float ge[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float d = te[e] * me[e] - oe[e] * me[e];
+                    s += (double)d * (double)d;
+                    ge[e] = act_bwd((-(norm * d)) * me[e], oe[e], act);
+                    sb += (double)ge[e];
+                }
+                g4[h ? qb : q] = make_float4(ge[0], ge[1], ge[2], ge[3]);
             }
-            g4[q] = make_float4(ge[0], ge[1], ge[2], ge[3]);
         }
     } else {
         for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
@@ -1361,21 +1424,40 @@ __global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out,
             sb += (double)g;
         }
     }
-    s = block_sum_d(s, red);
-    if (threadIdx.x == 0) atomicAdd(loss_acc, s);
-    sb = block_sum_d(sb, red);
+    int parity = 0;
+    s = block_sum_d1(s, red, parity);
+    sb = block_sum_d1(sb, red, parity);
+    double *bp = part + (int64_t)c * S, *lp = part + (int64_t)C * S + (int64_t)c * S;
+    double *cl = part + 2 * (int64_t)C * S;   // per-channel losses
+    // hand-offs without fences (lrs_common.h, wt_store): write-through partials, drain, count
     if (threadIdx.x == 0) {
-        bpart[(int64_t)c * gridDim.x + blockIdx.x] = sb;
-        __threadfence();
-        last = atomicAdd(cnt + c, 1) == (int)gridDim.x - 1;
+        wt_store(bp + blockIdx.x, sb);
+        wt_store(lp + blockIdx.x, s);
+        wt_drain();
+        last = agent_add(cnt + c, 1) == S - 1;
     }
     __syncthreads();
-    if (last && threadIdx.x == 0) {
-        __threadfence();
-        double t = 0.0;
-        for (unsigned k = 0; k < gridDim.x; ++k) t += bpart[(int64_t)c * gridDim.x + k];
-        gbias[c] = (float)t;
-        cnt[c] = 0;
+    if (!last) return;
+    // the channel's partials, summed by the whole workgroup in a fixed tree (S <= 64): deterministic
+    const int t = threadIdx.x;
+    double tb = t < S ? wt_load(bp + t) : 0.0, tl = t < S ? wt_load(lp + t) : 0.0;
+    tb = block_sum_d1(tb, red, parity);
+    tl = block_sum_d1(tl, red, parity);
+    if (t == 0) {
+        gbias[c] = (float)tb;
+        agent_store(cnt + c, 0);
+        wt_store(cl + c, tl);
+        wt_drain();
+        last = agent_add(cnt + C, 1) == C - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    double tot = 0.0;
+    for (int k = t; k < C; k += blockDim.x) tot += wt_load(cl + k);
+    tot = block_sum_d1(tot, red, parity);
+    if (t == 0) {
+        *loss_acc += tot;
+        agent_store(cnt + C, 0);
     }
 }
 

@@ -869,12 +869,13 @@ int mse_head(lrs_dipnet *net, const float *out, const float *target, const float
     float *gz = net->f(N.gz_off);
     const int64_t P = N.P;
     const int vec = (P % 4 == 0 && al16(out) && al16(target) && (!mask || al16(mask)) && al16(gz)) ? 1 : 0;
-    int64_t S = (512 + N.C - 1) / N.C;
-    S = std::max<int64_t>(1, std::min<int64_t>(S, (P + 1023) / 1024));
+    int64_t S = bn_split(P);   // ~4096 pixels per workgroup
     int64_t chunk = (P + S - 1) / S;
     if (vec) chunk = (chunk + 3) & ~(int64_t)3;
     S = (P + chunk - 1) / chunk;
-    if (chunk > INT32_MAX || (int64_t)N.C * S > bn_part_doubles(N.C, P)) return LRS_E_UNSUPPORTED;
+    // partials: bias [C][S], loss [C][S], channel losses [C]  (bn_part_doubles = 3 C bn_split(P))
+    if (chunk > INT32_MAX || P > INT32_MAX || 2 * (int64_t)N.C * S + N.C > bn_part_doubles(N.C, P))
+        return LRS_E_UNSUPPORTED;
     hipLaunchKernelGGL(k_mse_head, dim3((unsigned)S, (unsigned)N.C), dim3(256), 0, st, out, target, mask, N.C, P,
                        (int)chunk, vec, N.d.act, gz, net->loss_acc(), net->bnpart(), net->headcnt(),
                        net->grads + N.b_off);
@@ -1142,8 +1143,8 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     bytes += (size_t)round_up((int64_t)((net->n_prep > 0 ? net->n_prep : 1) * sizeof(ConvPrep)), 256);
     net->head_fusable = net->nodes.back().d.kind == LRS_NODE_CONV && net->nodes.back().d.bn == 0 &&
                         net->nodes.back().C <= 65535;
-    net->headcnt_off_bytes = (int64_t)bytes;
-    bytes += (size_t)round_up((int64_t)net->nodes.back().C * 4, 256);
+    net->headcnt_off_bytes = (int64_t)bytes;   // C per-channel counters + the channel counter
+    bytes += (size_t)round_up((int64_t)(net->nodes.back().C + 1) * 4, 256);
     net->misc_off_bytes = (int64_t)bytes;
     bytes += 256;
     net->ws_bytes = bytes;
@@ -1220,7 +1221,7 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
     if (e == hipSuccess && !prep.empty())
         e = hipMemcpy(net->prep(), prep.data(), sizeof(ConvPrep) * prep.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(net->misc_off_bytes + net->ws, 0, 256);
-    if (e == hipSuccess) e = hipMemset(net->headcnt(), 0, sizeof(int) * net->nodes.back().C);
+    if (e == hipSuccess) e = hipMemset(net->headcnt(), 0, sizeof(int) * (net->nodes.back().C + 1));
     return e == hipSuccess ? LRS_OK : (int)e;
 }
 

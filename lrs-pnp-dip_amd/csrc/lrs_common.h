@@ -19,6 +19,30 @@ __device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
 
 __host__ __device__ constexpr int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
+// In-launch hand-off of small partials to a "last arriver" workgroup without fences (gfx950: 8
+// XCDs with private L2s; MI355X_MICROARCH.md, visibility table row 1): the payload is stored
+// write-through (global_store sc1), the storing wave drains it (s_waitcnt vmcnt(0)), ONE lane then
+// adds to an agent-scope counter; the workgroup whose add returned count - 1 reads the payload with
+// sc1 loads only (they bypass the stale-able L1).  __threadfence() would instead write back the
+// whole XCD L2 per workgroup (buffer_wbl2 sc1): 2.6x slower on the DIP loss head.
+typedef __attribute__((address_space(1))) unsigned long long lrs_gu64;
+typedef __attribute__((address_space(1))) int lrs_gi32;
+__device__ __forceinline__ void wt_store(double *p, double v) {
+    __hip_atomic_store((lrs_gu64 *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double wt_load(const double *p) {
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((lrs_gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ int agent_add(int *p, int v) {
+    return __hip_atomic_fetch_add((lrs_gi32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void agent_store(int *p, int v) {
+    __hip_atomic_store((lrs_gi32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace lrs
 
 #define LRS_CHECK_LAUNCH()                                       \

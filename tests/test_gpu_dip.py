@@ -210,6 +210,9 @@ def test_sigma_max(L):
     sig, sc = sigma_max([m.cuda() for m in mats])
     ref = torch.tensor([float(torch.linalg.svdvals(m.double())[0]) for m in mats])
     np.testing.assert_allclose(sig.cpu().double().numpy(), ref.numpy(), rtol=2e-6)
+    # exact up to the float32 rounding of sigma: within one float32 ulp of the fp64 SVD value
+    r32 = ref.numpy().astype(np.float32)
+    assert (np.abs(sig.cpu().numpy() - r32) <= np.spacing(r32)).all(), (sig.cpu().numpy() - r32) / np.spacing(r32)
     np.testing.assert_allclose(sc.cpu().numpy(), np.maximum(1.0, sig.cpu().numpy()))
 
 

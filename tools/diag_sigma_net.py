@@ -52,4 +52,4 @@ for mk in marks:
     for i in range(n):
         t0 = p[i, 0]
         print(f"  conv {i:2d} {tuple(mats[i].shape)} sigma {sv[i]:.4f}: load {(p[i, 1] - t0) / 100:6.1f} us  "
-              f"lanczos {(p[i, 2] - p[i, 1]) / 100:6.1f} us (k={int(p[i, 4])})  final {(p[i, 3] - p[i, 2]) / 100:5.1f} us")
+              f"lanczos {(p[i, 2] - p[i, 1]) / 100:6.1f} us (k={int(p[i, 4])}, checks {p[i, 5] / 100:6.1f} us = {int(p[i, 6])} clk)  final {(p[i, 3] - p[i, 2]) / 100:5.1f} us")
