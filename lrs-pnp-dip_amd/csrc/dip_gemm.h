@@ -509,6 +509,7 @@ struct PwArgs {
     const float *bias;
     int M, Kp32, ldsrow, accum;
     int dbg;   // diagnostics only (LRS_PW_DBG): 1 no C stores, 2 no A loads, 4 no B loads
+    int act;   // activation applied after the bias (a conv without BN: its act in the epilogue)
 };
 
 inline int pw_ldsrow(int Kp32) {   // bytes; Kp32 * 2 rounded up to 16 mod 256
@@ -628,6 +629,7 @@ __global__ __launch_bounds__(256) void k_pw(PwArgs a) {
                     const float4 o = *reinterpret_cast<const float4 *>(c);
                     v.x = o.x + v.x; v.y = o.y + v.y; v.z = o.z + v.z; v.w = o.w + v.w;
                 }
+                if (a.act) { v.x = act_fwd(v.x, a.act); v.y = act_fwd(v.y, a.act); v.z = act_fwd(v.z, a.act); v.w = act_fwd(v.w, a.act); }
                 *reinterpret_cast<float4 *>(c) = v;
             } else {
                 const float vv[4] = {v.x, v.y, v.z, v.w};
@@ -636,6 +638,7 @@ __global__ __launch_bounds__(256) void k_pw(PwArgs a) {
                     float x = vv[u];
                     if (a.bias) x = x + bs;
                     if (a.accum) x = c[u] + x;
+                    if (a.act) x = act_fwd(x, a.act);
                     c[u] = x;
                 }
             }

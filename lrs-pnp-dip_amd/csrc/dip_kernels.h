@@ -959,6 +959,180 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd1(BnBwdArgs a) {
     bn_bwd_apply_body(a, c, 0, t, redf, st_s);
 }
 
+// ---- one workgroup per channel, the channel held in registers (P <= 4096 NQ, float4 path) ----
+// For the mid-size maps (98^2, 196^2 in configs[2]) the two-launch S-way split (statistics, then
+// apply, each re-reading the channel) costs more than one 1024-thread workgroup per channel that
+// reads every value once: thread t holds the float4 quads t + 1024 u, u < NQ.  The statistics are
+// the same fp64 shifted sums (K = z[c][0]) as k_bn_stats / k_bn_bwd_stats; only their summation
+// order differs.
+constexpr int kBnRegMaxQ = 10;   // 40960 pixels
+
+template <int NQ>
+__device__ __forceinline__ bool bnr_ok(int P, int u) { return threadIdx.x + u * kBn1Threads < (unsigned)(P >> 2); }
+
+// forward: z = (split-K partials summed in k_gemm_reduce's order + bias) or z as stored; then
+// BN statistics, normalisation, affine (Lipschitz rescale), activation.  part == nullptr: z given.
+template <int NQ>
+__global__ __launch_bounds__(kBn1Threads) void k_bn_fwd_r(const float *__restrict__ part, int nsplit,
+                                                          const float *__restrict__ bias, BnArgs a) {
+    __shared__ double red[2 * kBn1Threads / 64];
+    __shared__ float redf[kBn1Threads / 64];
+    __shared__ float st_s[3];
+    const int c = blockIdx.y, t = threadIdx.x;
+    const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
+    float4 zv[NQ];
+    float4 *z4 = reinterpret_cast<float4 *>(const_cast<float *>(a.z) + off);
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+        zv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!bnr_ok<NQ>(a.P, u)) continue;
+        const int q = t + u * kBn1Threads;
+        if (!part) {
+            zv[u] = z4[q];
+            continue;
+        }
+        // acc[e] = the splits e, e + 8, ... in increasing order (k_gemm_reduce's order); the loads of
+        // one group of 8 are predicated, not indexed, so acc stays in registers
+        float4 acc[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int z0 = 0; z0 < nsplit; z0 += 8) {
+            float4 p[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                p[e] = z0 + e < nsplit ? reinterpret_cast<const float4 *>(part + (int64_t)(z0 + e) * MN + off)[q]
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (z0 + e < nsplit) {
+                    acc[e].x += p[e].x; acc[e].y += p[e].y; acc[e].z += p[e].z; acc[e].w += p[e].w;
+                }
+        }
+        float4 v;
+        v.x = ((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x)) + ((acc[4].x + acc[5].x) + (acc[6].x + acc[7].x));
+        v.y = ((acc[0].y + acc[1].y) + (acc[2].y + acc[3].y)) + ((acc[4].y + acc[5].y) + (acc[6].y + acc[7].y));
+        v.z = ((acc[0].z + acc[1].z) + (acc[2].z + acc[3].z)) + ((acc[4].z + acc[5].z) + (acc[6].z + acc[7].z));
+        v.w = ((acc[0].w + acc[1].w) + (acc[2].w + acc[3].w)) + ((acc[4].w + acc[5].w) + (acc[6].w + acc[7].w));
+        if (bias) {
+            const float b = bias[c];
+            v.x = v.x + b; v.y = v.y + b; v.z = v.z + b; v.w = v.w + b;
+        }
+        zv[u] = v;
+        z4[q] = v;
+    }
+    if (t == 0) st_s[2] = zv[0].x;
+    __syncthreads();
+    const double K = (double)st_s[2];
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < NQ; ++u)
+        if (bnr_ok<NQ>(a.P, u)) {
+            const double d0 = (double)zv[u].x - K, d1 = (double)zv[u].y - K, d2 = (double)zv[u].z - K,
+                         d3 = (double)zv[u].w - K;
+            s1 += d0; s2 += d0 * d0;
+            s1 += d1; s2 += d1 * d1;
+            s1 += d2; s2 += d2 * d2;
+            s1 += d3; s2 += d3 * d3;
+        }
+    int par = 0;
+    s1 = block_sum_d1(s1, red, par);
+    s2 = block_sum_d1(s2, red, par);
+    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    if (t == 0) {
+        const double m = s1 / a.P;
+        double var = s2 / a.P - m * m;
+        if (var < 0.0) var = 0.0;
+        const float m32 = (float)(K + m);
+        const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
+        st_s[0] = m32;
+        st_s[1] = is32;
+        a.mean[c] = m32;
+        a.invstd[c] = is32;
+        if (a.run_mean) {
+            const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
+            a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
+            a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+        }
+    }
+    __syncthreads();
+    const float m32 = st_s[0], is32 = st_s[1];
+    const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
+    float4 *y4 = reinterpret_cast<float4 *>(a.y + off);
+#pragma unroll
+    for (int u = 0; u < NQ; ++u)
+        if (bnr_ok<NQ>(a.P, u)) {
+            const float4 v = zv[u];
+            y4[t + u * kBn1Threads] =
+                make_float4(act_fwd((v.x - m32) * is32 * gm + bt, a.act), act_fwd((v.y - m32) * is32 * gm + bt, a.act),
+                            act_fwd((v.z - m32) * is32 * gm + bt, a.act), act_fwd((v.w - m32) * is32 * gm + bt, a.act));
+        }
+}
+
+// backward (a.bn): g = act'(dL/dy) and x_hat held in registers, the three fp64 sums, then
+// dL/dz = k (g - mean(g) - x_hat mean(g x_hat)) (+= when accumulating), and the parameter grads
+template <int NQ>
+__global__ __launch_bounds__(kBn1Threads) void k_bn_bwd_r(BnBwdArgs a) {
+    __shared__ double red[2 * kBn1Threads / 64];
+    __shared__ float redf[kBn1Threads / 64];
+    __shared__ float st_s[2];
+    const int c = blockIdx.y, t = threadIdx.x;
+    const int64_t off = (int64_t)c * a.P;
+    const float4 *gy4 = reinterpret_cast<const float4 *>(a.gy + off), *y4 = reinterpret_cast<const float4 *>(a.y + off),
+                 *z4 = reinterpret_cast<const float4 *>(a.z + off);
+    const float m32 = a.mean[c], is32 = a.invstd[c];
+    float g[NQ][4], xh[NQ][4];
+    double sg = 0.0, sgx = 0.0, sx = 0.0;
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[u][e] = xh[u][e] = 0.0f;
+        if (!bnr_ok<NQ>(a.P, u)) continue;
+        const int q = t + u * kBn1Threads;
+        const float4 gv = gy4[q], yv = y4[q], zv = z4[q];
+        const float ge[4] = {gv.x, gv.y, gv.z, gv.w}, ye[4] = {yv.x, yv.y, yv.z, yv.w}, ze[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            g[u][e] = act_bwd(ge[e], ye[e], a.act);
+            xh[u][e] = (ze[e] - m32) * is32;
+            sg += (double)g[u][e];
+            sgx += (double)g[u][e] * (double)xh[u][e];
+            sx += (double)xh[u][e];
+        }
+    }
+    int par = 0;
+    sg = block_sum_d1(sg, red, par);
+    sgx = block_sum_d1(sgx, red, par);
+    sx = block_sum_d1(sx, red, par);
+    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    const float gm = a.gamma[c] / cs;
+    const float k = gm * is32;
+    if (t == 0) {
+        const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
+        st_s[0] = mg;
+        st_s[1] = mgx;
+        a.ggamma[c] = (float)sgx / cs;
+        a.gbeta[c] = (float)sg / cs;
+        if (a.gbias) a.gbias[c] = (float)((double)k * (sg - (double)a.P * mg - (double)mgx * sx));
+    }
+    __syncthreads();
+    const float mg = st_s[0], mgx = st_s[1];
+    float4 *gz4 = reinterpret_cast<float4 *>(a.gz + off);
+#pragma unroll
+    for (int u = 0; u < NQ; ++u)
+        if (bnr_ok<NQ>(a.P, u)) {
+            const int q = t + u * kBn1Threads;
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = k * (g[u][e] - mg - xh[u][e] * mgx);
+            float4 r = make_float4(o[0], o[1], o[2], o[3]);
+            if (a.accum) {
+                const float4 pv = gz4[q];
+                r = make_float4(pv.x + r.x, pv.y + r.y, pv.z + r.z, pv.w + r.w);
+            }
+            gz4[q] = r;
+        }
+}
+
 // ------------------------------------------------------------------------------------------
 // sigma_max of every conv weight W (rows x cols), batched: one conv per blockIdx.y.
 // Gram on the smaller side (m = min(rows, cols) <= 128) in fp64, exact products.

@@ -240,7 +240,7 @@ void wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, 
 
 // Pointwise conv product on k_pw (A: pre-split planes [3][M][lda], B: [K][N] fp32).
 int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, int K, int64_t N, float *C,
-              const float *bias, int accum, hipStream_t st) {
+              const float *bias, int accum, hipStream_t st, int act = 0) {
     if (M <= 0 || N <= 0) return LRS_OK;
     if (M > 256 || lda < K || lda % 16) return LRS_E_UNSUPPORTED;
     const int Kp32 = (int)round_up(lda, 32), ldsrow = pw_ldsrow(Kp32);
@@ -257,7 +257,7 @@ int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, 
     }
     if (Kp32 > 256 || (int64_t)K * N * 4 >= kOob || 3 * pstride * 2 >= kOob) return LRS_E_UNSUPPORTED;
     static const int dbg = getenv("LRS_PW_DBG") ? atoi(getenv("LRS_PW_DBG")) : 0;
-    const PwArgs a{A, pstride, lda, B, K, N, C, bias, M, Kp32, ldsrow, accum, dbg};
+    const PwArgs a{A, pstride, lda, B, K, N, C, bias, M, Kp32, ldsrow, accum, dbg, act};
     const dim3 grid((unsigned)((N + 63) / 64));
     switch ((M + 63) / 64) {
     case 1: hipLaunchKernelGGL(k_pw<1>, grid, dim3(256), lds, st, a); break;
@@ -273,13 +273,15 @@ inline bool pw_ok(const ConvGeom &g, int Cout) { return plain_unit(g) && Cout <=
 
 // y = conv(x) + bias.  Explicit (col != NULL): im2col + GEMM.  Implicit (col == NULL, wpre =
 // the weight planes from wprep): tap-major implicit GEMM.
+// act_pw: activation for the pointwise kernel's epilogue (a 1x1 conv without BN), applied only there.
 int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bias, int Cout, float *col, float *y,
-             float *part, int64_t part_cap, hipStream_t st, const __bf16 *wpre = nullptr, int *nsplit_out = nullptr) {
+             float *part, int64_t part_cap, hipStream_t st, const __bf16 *wpre = nullptr, int *nsplit_out = nullptr,
+             int act_pw = 0) {
     const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
     if (nsplit_out) *nsplit_out = 1;
     const float *B = x;
     if (plain_unit(g) && wpre)      // 1x1: pointwise kernel on the pre-split weights
-        return pw_launch(wpre, (int64_t)Cout * r16(g.Cin), r16(g.Cin), Cout, x, g.Cin, P, y, bias, 0, st);
+        return pw_launch(wpre, (int64_t)Cout * r16(g.Cin), r16(g.Cin), Cout, x, g.Cin, P, y, bias, 0, st, act_pw);
     if (!plain_unit(g) && !col) {   // implicit im2col
         if (!conv_implicit_ok(g, Cout) || !wpre) return LRS_E_UNSUPPORTED;
         const int kk = g.k * g.k, Cp = r16(g.Cin);
@@ -391,6 +393,30 @@ inline int64_t bn_part_doubles(int C, int64_t P) { return (int64_t)C * bn_split(
 
 inline bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
+// Register-resident one-workgroup-per-channel BN (k_bn_fwd_r / k_bn_bwd_r): float4 quads per
+// thread for a channel of P pixels, or 0 where the S-way split / the P <= 4096 kernels are used.
+// LRS_DIP_BNREG_MAX_P overrides the upper limit (tuning only; 0 disables).
+inline int bn_reg_q(int64_t P, bool vec) {
+    static const int64_t maxp = getenv("LRS_DIP_BNREG_MAX_P") ? atoll(getenv("LRS_DIP_BNREG_MAX_P"))
+                                                              : (int64_t)4 * kBn1Threads * kBnRegMaxQ;
+    if (!vec || P <= 4 * kBn1Threads || P > maxp || P > (int64_t)4 * kBn1Threads * kBnRegMaxQ) return 0;
+    const int q = (int)((P + 4 * kBn1Threads - 1) / (4 * kBn1Threads));
+    static const int qs[] = {2, 3, 4, 6, 8, 10};
+    for (int v : qs)
+        if (v >= q) return v;
+    return 0;
+}
+
+#define LRS_BNR_SWITCH(nq, K, ...)                                                                \
+    switch (nq) {                                                                                 \
+    case 2: hipLaunchKernelGGL(K<2>, __VA_ARGS__); break;                                         \
+    case 3: hipLaunchKernelGGL(K<3>, __VA_ARGS__); break;                                         \
+    case 4: hipLaunchKernelGGL(K<4>, __VA_ARGS__); break;                                         \
+    case 6: hipLaunchKernelGGL(K<6>, __VA_ARGS__); break;                                         \
+    case 8: hipLaunchKernelGGL(K<8>, __VA_ARGS__); break;                                         \
+    default: hipLaunchKernelGGL(K<10>, __VA_ARGS__); break;                                       \
+    }
+
 int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, float *mean, float *invstd, float *rm,
            float *rv, int C, int64_t P, int act, float eps, float mom, double *part, hipStream_t st, int lip = 1) {
     const int S = bn_split(P);
@@ -399,7 +425,10 @@ int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, floa
     if (vec) chunk = (chunk + 3) & ~3;
     BnArgs a{z, y, gamma, beta, mean, invstd, rm, rv, part, C, (int)P, S, chunk, gamma ? 1 : 0, act, eps, mom, lip,
              vec};
-    if (gamma && S == 1) {
+    if (const int nq = gamma ? bn_reg_q(P, vec) : 0) {
+        LRS_BNR_SWITCH(nq, k_bn_fwd_r, dim3(1, C), dim3(kBn1Threads), 0, st, (const float *)nullptr, 0,
+                       (const float *)nullptr, a);
+    } else if (gamma && S == 1) {
         hipLaunchKernelGGL(k_bn_fwd1, dim3(1, C), dim3(kBn1Threads), 0, st, a);
     } else {
         if (gamma) hipLaunchKernelGGL(k_bn_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
@@ -418,7 +447,9 @@ int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, 
     if (vec) chunk = (chunk + 3) & ~3;
     BnBwdArgs a{gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, part, C, (int)P, S, chunk,
                 gamma ? 1 : 0, act, lip, accum, vec};
-    if ((gamma || gbias) && S == 1) {
+    if (const int nq = gamma ? bn_reg_q(P, vec) : 0) {
+        LRS_BNR_SWITCH(nq, k_bn_bwd_r, dim3(1, C), dim3(kBn1Threads), 0, st, a);
+    } else if ((gamma || gbias) && S == 1) {
         hipLaunchKernelGGL(k_bn_bwd1, dim3(1, C), dim3(kBn1Threads), 0, st, a);
     } else {
         if (gamma || gbias) hipLaunchKernelGGL(k_bn_bwd_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
@@ -826,12 +857,26 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
             __bf16 *wp = N.wpre_off >= 0 ? (__bf16 *)net->f(N.wpre_off) : nullptr;
             // a BN channel that fits one workgroup finishes the conv's split-K sum itself (k_reduce_bn1)
             const bool fuse = bn && N.P <= 4 * kBn1Threads && bn_split(N.P) == 1;
+            // ... and so does the register-resident per-channel kernel for mid-size maps (k_bn_fwd_r)
+            const int nq = bn ? bn_reg_q(N.P, N.P % 4 == 0 && al16(z) && al16(out) && al16(net->f(net->part_off))) : 0;
+            // a 1x1 conv without BN applies its activation in the pointwise kernel's epilogue
+            const bool act_in_pw = !bn && plain_unit(N.g) && wp;
             int nsplit = 1;
             rc = conv_fwd(N.g, net->tensor(N.d.in0, x), w, net->params + N.b_off, N.C,
                           N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st, wp,
-                          fuse ? &nsplit : nullptr);
+                          (fuse || nq) ? &nsplit : nullptr, act_in_pw ? N.d.act : 0);
             if (rc) return rc;
-            if (fuse && nsplit > 1) {
+            if (act_in_pw) {
+                rc = LRS_OK;
+            } else if (nq) {
+                const BnArgs a{z, out, net->params + N.gm_off, net->params + N.bt_off, net->f(N.mean_off),
+                               net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C, nullptr, N.C,
+                               (int)N.P, 1, (int)N.P, 1, N.d.act, 1e-5f, 0.1f, lip, 1};
+                const float *pp = nsplit > 1 ? (const float *)net->f(net->part_off) : nullptr;
+                LRS_BNR_SWITCH(nq, k_bn_fwd_r, dim3(1, N.C), dim3(kBn1Threads), 0, st, pp, nsplit,
+                               (const float *)(net->params + N.b_off), a);
+                rc = LRS_OK;
+            } else if (fuse && nsplit > 1) {
                 const BnArgs a{z, out, net->params + N.gm_off, net->params + N.bt_off, net->f(N.mean_off),
                                net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C, nullptr, N.C,
                                (int)N.P, 1, (int)N.P, 1, N.d.act, 1e-5f, 0.1f, lip, 0};
