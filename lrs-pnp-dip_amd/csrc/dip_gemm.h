@@ -134,7 +134,7 @@ struct LdDense {
 };
 
 // source index of padded / upsampled coordinate u (extent n upsampled), -1 for a zero pad
-__device__ __forceinline__ int conv_src(int u, int n, int mode, int up) {
+__host__ __device__ __forceinline__ int conv_src(int u, int n, int mode, int up) {
     if (mode == LRS_PAD_REFLECT) {
         u = u < 0 ? -u : u;
         u = u >= n ? 2 * (n - 1) - u : u;

@@ -1068,6 +1068,67 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd_r(const float *__restric
         }
 }
 
+// Split-K finish + BatchNorm(+act) backward of one channel in one launch (P <= 4096: four values per
+// thread, any P): dL/dy = the sum of the data-gradient GEMM's split-K partials (k_gemm_reduce's
+// order; dL/dy itself is not stored: only this kernel reads it), then k_bn_bwd_r's arithmetic.
+// Replaces k_gemm_reduce + k_bn_bwd1 below a small-map conv's data gradient.
+__global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__restrict__ part, int nsplit,
+                                                                BnBwdArgs a) {
+    __shared__ double red[2 * kBn1Threads / 64];
+    __shared__ float redf[kBn1Threads / 64];
+    __shared__ float st_s[2];
+    const int c = blockIdx.y, t = threadIdx.x;
+    const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
+    const float m32 = a.mean[c], is32 = a.invstd[c];
+    float g[4], xh[4];
+    double sg = 0.0, sgx = 0.0, sx = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = t + u * kBn1Threads;
+        g[u] = xh[u] = 0.0f;
+        if (i >= a.P) continue;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int z0 = 0; z0 < nsplit; z0 += 8) {
+            float p[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) p[e] = z0 + e < nsplit ? part[(int64_t)(z0 + e) * MN + off + i] : 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (z0 + e < nsplit) acc[e] += p[e];
+        }
+        const float gy = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+        g[u] = act_bwd(gy, a.y[off + i], a.act);
+        xh[u] = (a.z[off + i] - m32) * is32;
+        sg += (double)g[u];
+        sgx += (double)g[u] * (double)xh[u];
+        sx += (double)xh[u];
+    }
+    int par = 0;
+    sg = block_sum_d1(sg, red, par);
+    sgx = block_sum_d1(sgx, red, par);
+    sx = block_sum_d1(sx, red, par);
+    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    const float gm = a.gamma[c] / cs;
+    const float k = gm * is32;
+    if (t == 0) {
+        const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
+        st_s[0] = mg;
+        st_s[1] = mgx;
+        a.ggamma[c] = (float)sgx / cs;
+        a.gbeta[c] = (float)sg / cs;
+        if (a.gbias) a.gbias[c] = (float)((double)k * (sg - (double)a.P * mg - (double)mgx * sx));
+    }
+    __syncthreads();
+    const float mg = st_s[0], mgx = st_s[1];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = t + u * kBn1Threads;
+        if (i >= a.P) continue;
+        const float v = k * (g[u] - mg - xh[u] * mgx);
+        a.gz[off + i] = a.accum ? a.gz[off + i] + v : v;
+    }
+}
+
 // backward (a.bn): g = act'(dL/dy) and x_hat held in registers, the three fp64 sums, then
 // dL/dz = k (g - mean(g) - x_hat mean(g x_hat)) (+= when accumulating), and the parameter grads
 template <int NQ>

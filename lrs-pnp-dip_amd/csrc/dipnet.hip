@@ -15,6 +15,7 @@
 
 #include "dip_kernels.h"
 #include "dip_gemm.h"
+#include "dip_sm.h"
 
 using namespace lrs;
 
@@ -169,6 +170,102 @@ inline int up_eff_k(const ConvGeom &g) {
     if (g.k == 2 && g.pad == 0) return 3;
     return 0;
 }
+// ---- small-map convs on k_conv_sm (dip_sm.h) ------------------------------------------------
+// A conv runs there when it is not 1x1, k <= 3 and its output map is below implicit_min_pixels()
+// (the maps that had the explicit im2col path).  LRS_DIP_SM=0 keeps the explicit path (A/B only).
+inline bool sm_enabled() {
+    static const bool v = !getenv("LRS_DIP_SM") || atoi(getenv("LRS_DIP_SM")) != 0;
+    return v;
+}
+
+// 64 x 64 tiles; split K so that the grid has ~sm_target() workgroups (k per split a multiple of
+// 64).  LRS_DIP_SM_WG overrides the target (tuning only).
+inline int64_t sm_target() {
+    static const int64_t v = getenv("LRS_DIP_SM_WG") ? std::max(1LL, atoll(getenv("LRS_DIP_SM_WG"))) : 640;
+    return v;
+}
+Split sm_split(int M, int N, int K) {
+    const int64_t T = (int64_t)((M + 63) / 64) * ((N + 63) / 64), W = sm_target();
+    int64_t kc = round_up(std::max<int64_t>(1, ((int64_t)K * T + W - 1) / W), kSmK);
+    if (kc > K) kc = round_up(K, kSmK);
+    int S = (int)((K + kc - 1) / kc);
+    kc = round_up((K + S - 1) / S, kSmK);
+    S = (int)((K + kc - 1) / kc);
+    return {S, (int)kc, false};
+}
+
+int64_t sm_part_floats(int M, int N, int K) {
+    const Split s = sm_split(M, N, K);
+    return s.S > 1 ? (int64_t)s.S * M * N : 0;
+}
+
+// C (+)= A B on k_conv_sm; split-K partials summed by k_gemm_reduce unless nsplit_out is given
+// (the caller then finishes the sum, e.g. k_reduce_bn1)
+template <class LB>
+int sm_launch(const SmPre &la, const LB &lb, float *C, const float *bias, int M, int N, int K, int accum, float *part,
+              int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr) {
+    if (M <= 0 || N <= 0) return LRS_OK;
+    const Split s = sm_split(M, N, K);
+    if (nsplit_out) *nsplit_out = s.S;
+    GemmArgs g{nullptr, nullptr, C, bias, nullptr, M, N, K, s.kchunk, accum};
+    if (s.S > 1) {
+        if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
+        g.C = part;
+    }
+    hipLaunchKernelGGL((k_conv_sm<LB>), dim3((N + 63) / 64, (M + 63) / 64, s.S), dim3(256), 0, st, g, la, lb);
+    if (s.S > 1 && !nsplit_out) {
+        const int64_t MN = (int64_t)M * N;
+        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M, N,
+                           bias, nullptr, accum, C);
+    }
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+// The data-gradient gather table of a small-map conv: for tap (ty, tx) and input pixel q, the
+// byte offsets (within a dL/dz plane) of the <= 2 x 2 output pixels that read q through it (the
+// products of the per-dimension lists), kOob-padded; [kk][Q] int4.  Empty where sm_adj_dim fails.
+std::vector<int> sm_adj_table(const ConvGeom &g);
+
+// The conv's adjoint along one dimension: for tap t and source coordinate q, the output
+// coordinates o with src(o, t) = q (reflection / zero pad, stride, x2 upsample), in increasing
+// order, at most 2 (-1 = none).  False where some list would need more (the caller then keeps the
+// explicit data gradient).
+bool sm_adj_dim(int n_src, int n_up, int n_out, int k, int stride, int pad, int mode, int up, short *L) {
+    for (int i = 0; i < k * n_src * 2; ++i) L[i] = -1;
+    for (int o = 0; o < n_out; ++o)
+        for (int t = 0; t < k; ++t) {
+            const int q = conv_src(o * stride + t - pad, n_up, mode, up);
+            if (q < 0) continue;
+            short *e = L + (t * n_src + q) * 2;
+            if (e[0] < 0) e[0] = (short)o;
+            else if (e[1] < 0) e[1] = (short)o;
+            else return false;
+        }
+    return true;
+}
+
+std::vector<int> sm_adj_table(const ConvGeom &g) {
+    std::vector<short> Ly((size_t)2 * g.k * g.Hs), Lx((size_t)2 * g.k * g.Ws);
+    if (!sm_adj_dim(g.Hs, g.Hu, g.Ho, g.k, g.stride, g.pad, g.pad_mode, g.up, Ly.data()) ||
+        !sm_adj_dim(g.Ws, g.Wu, g.Wo, g.k, g.stride, g.pad, g.pad_mode, g.up, Lx.data()))
+        return {};
+    const int Q = g.Hs * g.Ws;
+    std::vector<int> t((size_t)4 * g.k * g.k * Q, kOob);
+    for (int ty = 0; ty < g.k; ++ty)
+        for (int tx = 0; tx < g.k; ++tx)
+            for (int q = 0; q < Q; ++q) {
+                const int qy = q / g.Ws, qx = q % g.Ws;
+                int *e = t.data() + 4 * ((int64_t)(ty * g.k + tx) * Q + q);
+                for (int a = 0; a < 2; ++a)
+                    for (int b = 0; b < 2; ++b) {
+                        const int oy = Ly[(ty * g.Hs + qy) * 2 + a], ox = Lx[(tx * g.Ws + qx) * 2 + b];
+                        if (oy >= 0 && ox >= 0) e[2 * a + b] = 4 * (oy * g.Wo + ox);
+                    }
+            }
+    return t;
+}
+
 int64_t conv_part_floats(const ConvGeom &g, int Cout) {
     const int P = g.Ho * g.Wo, kk = g.k * g.k, Kc = g.Cin * kk;
     int64_t m = gemm_part_floats(Cout, P, Kc);                       // forward
@@ -181,6 +278,7 @@ int64_t conv_part_floats(const ConvGeom &g, int Cout) {
     const int Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad);
     m = std::max(m, s3_part_floats(g.Cin, Qp, kk * r16(Cout)));
     if (const int ke = up_eff_k(g)) m = std::max(m, s3_part_floats(g.Cin, g.Hs * g.Ws, ke * ke * r16(Cout)));
+    m = std::max(m, std::max(sm_part_floats(Cout, P, kk * r16(g.Cin)), sm_part_floats(g.Cin, g.Hs * g.Ws, kk * r16(Cout))));
     return m;
 }
 
@@ -783,6 +881,10 @@ struct lrs_dipnet {
         int64_t wpre_off = -1;        // implicit convs: bf16 weight planes (wprep)
         int64_t gz_off = -1;          // conv: dL/dz (read by the side-stream weight gradient)
         int sn_index = -1;            // position in the spectral-norm table
+        bool sm = false;              // small map: forward / data gradient on k_conv_sm (dip_sm.h)
+        bool sm_dgrad = false;        // ... data gradient through the adjoint lists below
+        int64_t adj_off = -1;         // the lists in the workspace (shorts, sm_adj_dim)
+        std::vector<int> adj;         // host copy (sm_adj_table), uploaded at bind
     };
     std::vector<Node> nodes;
     int C0 = 0, H = 0, W = 0;
@@ -862,9 +964,17 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
             // a 1x1 conv without BN applies its activation in the pointwise kernel's epilogue
             const bool act_in_pw = !bn && plain_unit(N.g) && wp;
             int nsplit = 1;
-            rc = conv_fwd(N.g, net->tensor(N.d.in0, x), w, net->params + N.b_off, N.C,
-                          N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st, wp,
-                          (fuse || nq) ? &nsplit : nullptr, act_in_pw ? N.d.act : 0);
+            if (N.sm) {   // small map: implicit GEMM on k_conv_sm, no col written
+                const int kk = N.g.k * N.g.k, Cp = r16(N.g.Cin);
+                rc = sm_launch(SmPre{wp, (int64_t)N.C * kk * Cp, kk * Cp, N.C},
+                               SmFwd{net->tensor(N.d.in0, x), N.g.Cin * N.g.Hs * N.g.Ws * 4, N.g, Cp, nullptr}, z,
+                               net->params + N.b_off, N.C, (int)N.P, kk * Cp, 0, net->f(net->part_off), net->part_cap, st,
+                               (fuse || nq) ? &nsplit : nullptr);
+            } else {
+                rc = conv_fwd(N.g, net->tensor(N.d.in0, x), w, net->params + N.b_off, N.C,
+                              N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st,
+                              wp, (fuse || nq) ? &nsplit : nullptr, act_in_pw ? N.d.act : 0);
+            }
             if (rc) return rc;
             if (act_in_pw) {
                 rc = LRS_OK;
@@ -965,6 +1075,10 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
     // gradient buffers: the first contribution to a tensor writes, later ones accumulate
     std::vector<char> written(n + 1, 0);
     written[n] = 1;
+    // a small-map data gradient may leave dL/dy of the next node as split-K partials, finished by
+    // that node's k_reduce_bn_bwd1 (pend = the partials, pend_S their count)
+    const float *pend = nullptr;
+    int pend_S = 0;
     for (int i = n - 1; i >= 0; --i) {
         auto &N = net->nodes[i];
         float *gout = net->f(N.grad_off);
@@ -975,7 +1089,13 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
             const bool bn = N.d.bn != 0;
             float *z = bn ? net->f(N.z_off) : outp;
             float *gz = net->f(N.gz_off);
-            if (!(head_done && i == n - 1)) {   // else k_mse_head wrote gz and the bias gradient
+            if (pend) {
+                const BnBwdArgs a{nullptr, outp, z, net->params + N.gm_off, net->f(N.mean_off), net->f(N.istd_off), gz,
+                                  net->grads + N.gm_off, net->grads + N.bt_off, net->grads + N.b_off, nullptr, N.C,
+                                  (int)N.P, 1, (int)N.P, 1, N.d.act, lip, 0, 0};
+                hipLaunchKernelGGL(k_reduce_bn_bwd1, dim3(1, N.C), dim3(kBn1Threads), 0, st, pend, pend_S, a);
+                pend = nullptr;
+            } else if (!(head_done && i == n - 1)) {   // else k_mse_head wrote gz and the bias gradient
                 rc = bn_bwd(gout, outp, z, bn ? net->params + N.gm_off : nullptr, net->f(N.mean_off),
                             net->f(N.istd_off), gz, bn ? net->grads + N.gm_off : nullptr,
                             bn ? net->grads + N.bt_off : nullptr, net->grads + N.b_off, N.C, N.P, N.d.act,
@@ -996,10 +1116,34 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
                 if (e != hipSuccess) return (int)e;
                 ws = net->side;
             }
+            if (N.sm) {   // the forward gathered inside k_conv_sm: the col for the weight gradient now
+                const int P = N.g.Ho * N.g.Wo;
+                const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min<int64_t>(N.Kc, 65535));
+                hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, ws, net->tensor(t, x), N.g, net->f(N.col_off));
+            }
             rc = conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, nullptr, net->grads + N.w_off, nullptr,
                           net->f(net->part2_off), net->part_cap, ws, 0, N.col_off < 0);
             if (rc) return rc;
-            if (gx) {
+            if (gx && N.sm_dgrad) {   // gx = the adjoint gather of dL/dz on k_conv_sm
+                const auto &g = N.g;
+                const int kk = g.k * g.k, Cop = r16(N.C);
+                const __bf16 *wd = (const __bf16 *)net->f(N.wpre_off) + wprep_fwd_elems(g, N.C);
+                // the next node (t - 1 = i - 1, this tensor's only other writer would come before it)
+                // finishes the split-K sum inside its BN backward when that fits one workgroup
+                const auto &Np = net->nodes[t - 1];
+                const bool fuse_next = t == i && !written[t] && Np.d.kind == LRS_NODE_CONV && Np.d.bn &&
+                                       Np.P <= 4 * kBn1Threads && bn_split(Np.P) == 1 && !(head_done && t - 1 == n - 1);
+                int nsplit = 1;
+                rc = sm_launch(SmPre{wd, (int64_t)g.Cin * kk * Cop, kk * Cop, g.Cin},
+                               SmAdj{gz, (int)(N.C * N.P * 4), g, N.C, Cop, (const int4 *)net->f(N.adj_off), nullptr}, gx,
+                               nullptr, g.Cin, g.Hs * g.Ws, kk * Cop, written[t], net->f(net->part_off), net->part_cap, st,
+                               fuse_next ? &nsplit : nullptr);
+                if (rc) return rc;
+                if (fuse_next && nsplit > 1) {
+                    pend = net->f(net->part_off);
+                    pend_S = nsplit;
+                }
+            } else if (gx) {
                 rc = conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, gx, nullptr,
                               !plain_unit(N.g) ? net->f(net->dcol_off) : nullptr, net->f(net->part_off),
                               net->part_cap, st, written[t], N.col_off < 0,
@@ -1076,6 +1220,7 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     // concurrent sparse-coding kernel the second stream keeps the DIP its share of the chip
     // (configs[2] 4.73 -> 5.19 outer it/s); slower at 36^2 (1.03 -> 1.19 ms per step)
     net->fork_w = (int64_t)H * W >= 16384;
+    if (const char *e = getenv("LRS_DIP_FORK")) net->fork_w = atoi(e) != 0;   // tuning / A/B only
     int64_t pofs = 0, rofs = 0, ofs = 0, max_dz = 0, max_dcol = 0, part = 0, max_bnpart = 0;
     int n_sn = 0;
     for (int i = 0; i < n_nodes; ++i) {
@@ -1109,8 +1254,23 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
             }
             if (!plain_unit(N.g)) {
                 if (!(net->implicit && conv_implicit_ok(N.g, N.C) && N.P >= implicit_min_pixels())) {
+                    // col: the weight gradient's explicit im2col (written in the backward for a
+                    // small-map conv, whose forward gathers it inside k_conv_sm)
                     N.col_off = ofs;
                     ofs += align64(N.Kc * N.P);
+                    if (net->implicit && sm_enabled() && N.d.k <= 3 && conv_implicit_ok(N.g, N.C)) {
+                        N.sm = true;
+                        N.wpre_off = ofs;
+                        ofs += align64((wprep_elems(N.g, N.C) + 1) / 2);
+                        if (t0 > 0) {
+                            N.adj = sm_adj_table(N.g);
+                            N.sm_dgrad = !N.adj.empty();
+                            if (N.sm_dgrad) {
+                                N.adj_off = ofs;
+                                ofs += align64((int64_t)N.adj.size());
+                            }
+                        }
+                    }
                 } else {
                     N.wpre_off = ofs;
                     ofs += align64((wprep_elems(N.g, N.C) + 1) / 2);
@@ -1259,9 +1419,13 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
         __bf16 *wf = N.wpre_off >= 0 ? (__bf16 *)net->f(N.wpre_off) : nullptr;
         __bf16 *wd = (wf && N.d.in0 > 0) ? wf + wprep_fwd_elems(N.g, N.C) : nullptr;
         prep.push_back(ConvPrep{params + N.w_off, N.sn_index >= 0 ? net->f(N.wn_off) : nullptr, wf, wd, N.C, N.g.Cin,
-                                N.g.k * N.g.k, r16(N.g.Cin), r16(N.C), N.sn_index, N.g.k, wd ? up_eff_k(N.g) : 0});
+                                N.g.k * N.g.k, r16(N.g.Cin), r16(N.C), N.sn_index, N.g.k,
+                                (wd && !N.sm) ? up_eff_k(N.g) : 0});
     }
     hipError_t e = hipSuccess;
+    for (const auto &N : net->nodes)
+        if (e == hipSuccess && N.sm_dgrad)
+            e = hipMemcpy(net->f(N.adj_off), N.adj.data(), sizeof(int) * N.adj.size(), hipMemcpyHostToDevice);
     if (!tab.empty()) e = hipMemcpy(net->table(), tab.data(), sizeof(SnConv) * tab.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && !prep.empty())
         e = hipMemcpy(net->prep(), prep.data(), sizeof(ConvPrep) * prep.size(), hipMemcpyHostToDevice);

@@ -20,14 +20,15 @@ step = rows[a:b]
 t0 = int(step[0]["Start_Timestamp"])
 qkey = "Queue_Id" if "Queue_Id" in step[0] else ("Stream_Id" if "Stream_Id" in step[0] else None)
 busy = {}
-print(f"{'start':>8} {'dur':>7} {'q':>3} {'grid':>16}  kernel")
+print(f"{'start':>8} {'dur':>7} {'q':>3} {'s':>3} {'grid':>16}  kernel")
 for r in step:
     s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
     q = r.get(qkey, "?") if qkey else "?"
     busy[q] = busy.get(q, 0) + (e - s)
     grid = f"{r['Grid_Size_X']}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}"
     name = r["Kernel_Name"].replace("lrs::", "").split("(")[0][:70]
-    print(f"{s / 1e3:8.1f} {(e - s) / 1e3:7.1f} {q:>3} {grid:>16}  {name}")
+    sid = r.get("Stream_Id", "?")
+    print(f"{s / 1e3:8.1f} {(e - s) / 1e3:7.1f} {q:>3} {sid:>3} {grid:>16}  {name}")
 wall = int(rows[b]["Start_Timestamp"]) - t0
 print(f"step wall {wall / 1e3:.1f} us, {len(step)} kernels; busy per queue: "
       + ", ".join(f"{q}: {v / 1e3:.1f} us" for q, v in busy.items()))
