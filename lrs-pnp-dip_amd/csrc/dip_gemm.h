@@ -332,6 +332,7 @@ template <class L>
 struct HasPrepare {
     static constexpr bool value = false;
 };
+
 template <>
 struct HasPrepare<LdWgradTM> {
     static constexpr bool value = true;

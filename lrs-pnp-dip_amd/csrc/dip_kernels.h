@@ -970,6 +970,33 @@ constexpr int kBnRegMaxQ = 10;   // 40960 pixels
 template <int NQ>
 __device__ __forceinline__ bool bnr_ok(int P, int u) { return threadIdx.x + u * kBn1Threads < (unsigned)(P >> 2); }
 
+// quad q of a [C][P] tensor at channel offset off, summed over nsplit split-K partials (stride MN):
+// acc[e] = the splits e, e + 8, ... in increasing order (k_gemm_reduce's order); the loads of one
+// group of 8 are predicated, not indexed, so acc stays in registers
+__device__ __forceinline__ float4 splitk_sum4(const float *__restrict__ part, int nsplit, int64_t MN, int64_t off, int q) {
+    float4 acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z0 = 0; z0 < nsplit; z0 += 8) {
+        float4 p[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            p[e] = z0 + e < nsplit ? reinterpret_cast<const float4 *>(part + (int64_t)(z0 + e) * MN + off)[q]
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (z0 + e < nsplit) {
+                acc[e].x += p[e].x; acc[e].y += p[e].y; acc[e].z += p[e].z; acc[e].w += p[e].w;
+            }
+    }
+    float4 v;
+    v.x = ((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x)) + ((acc[4].x + acc[5].x) + (acc[6].x + acc[7].x));
+    v.y = ((acc[0].y + acc[1].y) + (acc[2].y + acc[3].y)) + ((acc[4].y + acc[5].y) + (acc[6].y + acc[7].y));
+    v.z = ((acc[0].z + acc[1].z) + (acc[2].z + acc[3].z)) + ((acc[4].z + acc[5].z) + (acc[6].z + acc[7].z));
+    v.w = ((acc[0].w + acc[1].w) + (acc[2].w + acc[3].w)) + ((acc[4].w + acc[5].w) + (acc[6].w + acc[7].w));
+    return v;
+}
+
 // forward: z = (split-K partials summed in k_gemm_reduce's order + bias) or z as stored; then
 // BN statistics, normalisation, affine (Lipschitz rescale), activation.  part == nullptr: z given.
 template <int NQ>
@@ -993,26 +1020,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd_r(const float *__restric
         }
         // acc[e] = the splits e, e + 8, ... in increasing order (k_gemm_reduce's order); the loads of
         // one group of 8 are predicated, not indexed, so acc stays in registers
-        float4 acc[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int z0 = 0; z0 < nsplit; z0 += 8) {
-            float4 p[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                p[e] = z0 + e < nsplit ? reinterpret_cast<const float4 *>(part + (int64_t)(z0 + e) * MN + off)[q]
-                                       : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                if (z0 + e < nsplit) {
-                    acc[e].x += p[e].x; acc[e].y += p[e].y; acc[e].z += p[e].z; acc[e].w += p[e].w;
-                }
-        }
-        float4 v;
-        v.x = ((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x)) + ((acc[4].x + acc[5].x) + (acc[6].x + acc[7].x));
-        v.y = ((acc[0].y + acc[1].y) + (acc[2].y + acc[3].y)) + ((acc[4].y + acc[5].y) + (acc[6].y + acc[7].y));
-        v.z = ((acc[0].z + acc[1].z) + (acc[2].z + acc[3].z)) + ((acc[4].z + acc[5].z) + (acc[6].z + acc[7].z));
-        v.w = ((acc[0].w + acc[1].w) + (acc[2].w + acc[3].w)) + ((acc[4].w + acc[5].w) + (acc[6].w + acc[7].w));
+        float4 v = splitk_sum4(part, nsplit, MN, off, q);
         if (bias) {
             const float b = bias[c];
             v.x = v.x + b; v.y = v.y + b; v.z = v.z + b; v.w = v.w + b;

@@ -21,7 +21,7 @@
 namespace lrs {
 
 constexpr int kSmK = 64;                 // k per LDS stage
-constexpr int kSmTabInts = 9 * 64 * 4;   // k <= 3: [tap][pixel][4 combos]
+constexpr int kSmTabInts = 9 * 64 * 4 + 16;   // k <= 3: [tap][pixel][4 combos] + per-tap flags
 
 struct SmImg {
     __bf16 v[3][64][kSmK];   // [plane][row][k], 128-B rows, 16-B chunks swizzled by sm_chunk
@@ -125,18 +125,25 @@ struct SmAdj {
     int Cout, Cop;
     const int4 *adj;
     const int *tab;
+    // + one flag per tap after the table: no second term anywhere in the tile -> the single-load path
     __device__ __forceinline__ void setup(int x0, int *smem) {
         const int kk = g.k * g.k, Q = g.Hs * g.Ws;
+        int *multi = smem + kk * 64 * 4;
         int4 e[3];
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
             const int i = threadIdx.x + 256 * u, kyx = i >> 6, q = x0 + (i & 63);
             e[u] = (kyx < kk && q < Q) ? adj[(int64_t)kyx * Q + q] : int4{kOob, kOob, kOob, kOob};
         }
+        if (threadIdx.x < kk) multi[threadIdx.x] = 0;
+        __syncthreads();
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
             const int i = threadIdx.x + 256 * u;
-            if ((i >> 6) < kk) *reinterpret_cast<int4 *>(smem + 4 * i) = e[u];
+            if ((i >> 6) < kk) {
+                *reinterpret_cast<int4 *>(smem + 4 * i) = e[u];
+                if ((e[u].y & e[u].z & e[u].w) != kOob) atomicOr(multi + (i >> 6), 1);
+            }
         }
         tab = smem;
     }
@@ -147,6 +154,11 @@ struct SmAdj {
         const __amdgpu_buffer_rsrc_t rs = s3_rsrc(GZ, gbytes);
         int4 o = int4{kOob, kOob, kOob, kOob};
         if (r0 < kend) o = *reinterpret_cast<const int4 *>(tab + 4 * (kyx * 64 + sm_row(j)));
+        if (r0 >= kend || !__builtin_amdgcn_readfirstlane(tab[g.k * g.k * 64 * 4 + kyx])) {   // one term per pixel
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = c0 + u < Cout ? s3_bload(rs, o.x, (c0 + u) * pb) : 0.0f;
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             float s = 0.0f;

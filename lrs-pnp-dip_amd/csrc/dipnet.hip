@@ -294,11 +294,11 @@ inline int64_t wprep_elems(const ConvGeom &g, int Cout) {
 // gemm().
 template <class LA, class LB>
 int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const float *div, int M, int N, int K,
-                 float *part, int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr) {
+                 float *part, int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr, int accum = 0) {
     if (M <= 0 || N <= 0) return LRS_OK;
     const Split s = choose_split(M, N, K, LRS_DIP_SPLIT_BF16, true);
     if (nsplit_out) *nsplit_out = s.S;
-    GemmArgs g{nullptr, nullptr, C, bias, div, M, N, K, s.kchunk, 0};
+    GemmArgs g{nullptr, nullptr, C, bias, div, M, N, K, s.kchunk, accum};
     if (s.S > 1) {
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
         g.C = part;
@@ -308,7 +308,7 @@ int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const 
     if (s.S > 1 && !nsplit_out) {
         const int64_t MN = (int64_t)M * N;
         hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M, N,
-                           bias, div, 0, C);
+                           bias, div, accum, C);
     }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
@@ -882,7 +882,7 @@ struct lrs_dipnet {
         int64_t gz_off = -1;          // conv: dL/dz (read by the side-stream weight gradient)
         int sn_index = -1;            // position in the spectral-norm table
         bool sm = false;              // small map: forward / data gradient on k_conv_sm (dip_sm.h)
-        bool sm_dgrad = false;        // ... data gradient through the adjoint lists below
+        bool sm_dgrad = false;        // ... data gradient through the adjoint table below
         int64_t adj_off = -1;         // the lists in the workspace (shorts, sm_adj_dim)
         std::vector<int> adj;         // host copy (sm_adj_table), uploaded at bind
     };
@@ -935,6 +935,13 @@ struct lrs_dipnet {
 namespace {
 
 int64_t align64(int64_t n) { return (n + 63) / 64 * 64; }   // floats (256 bytes)
+
+// Can node j's BN backward finish a split-K dL/dy itself (k_reduce_bn_bwd1: a conv with BN whose
+// channel fits one workgroup)?
+bool bn_bwd_fusable(const lrs_dipnet *net, int j) {
+    const auto &N = net->nodes[j];
+    return N.d.kind == LRS_NODE_CONV && N.d.bn && N.P <= 4 * kBn1Threads && bn_split(N.P) == 1;
+}
 
 int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_begin = false) {
     int rc;
@@ -1124,19 +1131,18 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
             rc = conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, nullptr, net->grads + N.w_off, nullptr,
                           net->f(net->part2_off), net->part_cap, ws, 0, N.col_off < 0);
             if (rc) return rc;
-            if (gx && N.sm_dgrad) {   // gx = the adjoint gather of dL/dz on k_conv_sm
+            if (gx && N.sm_dgrad) {   // gx = the adjoint gather of dL/dz on k_conv_sm, one GEMM
                 const auto &g = N.g;
                 const int kk = g.k * g.k, Cop = r16(N.C);
                 const __bf16 *wd = (const __bf16 *)net->f(N.wpre_off) + wprep_fwd_elems(g, N.C);
+                const SmPre la{wd, (int64_t)g.Cin * kk * Cop, kk * Cop, g.Cin};
+                const int4 *adj = (const int4 *)net->f(N.adj_off);
                 // the next node (t - 1 = i - 1, this tensor's only other writer would come before it)
                 // finishes the split-K sum inside its BN backward when that fits one workgroup
-                const auto &Np = net->nodes[t - 1];
-                const bool fuse_next = t == i && !written[t] && Np.d.kind == LRS_NODE_CONV && Np.d.bn &&
-                                       Np.P <= 4 * kBn1Threads && bn_split(Np.P) == 1 && !(head_done && t - 1 == n - 1);
+                const bool fuse_next = t == i && !written[t] && bn_bwd_fusable(net, t - 1) && !(head_done && t - 1 == n - 1);
                 int nsplit = 1;
-                rc = sm_launch(SmPre{wd, (int64_t)g.Cin * kk * Cop, kk * Cop, g.Cin},
-                               SmAdj{gz, (int)(N.C * N.P * 4), g, N.C, Cop, (const int4 *)net->f(N.adj_off), nullptr}, gx,
-                               nullptr, g.Cin, g.Hs * g.Ws, kk * Cop, written[t], net->f(net->part_off), net->part_cap, st,
+                rc = sm_launch(la, SmAdj{gz, (int)(N.C * N.P * 4), g, N.C, Cop, adj, nullptr}, gx, nullptr, g.Cin,
+                               g.Hs * g.Ws, kk * Cop, written[t], net->f(net->part_off), net->part_cap, st,
                                fuse_next ? &nsplit : nullptr);
                 if (rc) return rc;
                 if (fuse_next && nsplit > 1) {
