@@ -106,7 +106,11 @@ def make_problem(H, W, B, bb, K, seed):
     return unfold(obs), mask_matrix(mask, B), synthetic_dictionary(bb * bb, K, 0), clean
 
 
-def load_traffic(key):
+def load_traffic(key, profiled=True):
+    """HBM bytes of the committed PMC pass (profiles/r02/traffic.json); None for a configuration
+    other than the profiled default one."""
+    if not profiled:
+        return None
     try:
         return json.load(open(TRAFFIC_FILE)).get(key)
     except Exception:
@@ -248,10 +252,10 @@ def dip_flops_per_step(net):
     return tot
 
 
-def ista_entry(name, ista_ms, flops, traffic_key):
+def ista_entry(name, ista_ms, flops, traffic_key, profiled=True):
     achieved = flops / (ista_ms * 1e-3) / 1e12
     return {"kernel": name, "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": load_traffic(traffic_key),
+            "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": load_traffic(traffic_key, profiled),
             "flops_per_launch": flops, "ms_per_launch": ista_ms}
 
 
@@ -296,6 +300,7 @@ def main_dip(args, ctx):
             dip_ms = per[0][0]
             ista_ms = float(np.nanmean([v[1] for v in per[1:]]))
     flops = dip_flops_per_step(s.dip.net) * args.dip_steps
+    profiled = not (args.cube or args.bb or args.nit or args.K != 256 or args.dip_steps != 100)
     achieved = flops / (dip_ms * 1e-3) / 1e12
     n = bb * bb
     ista_flops = nit * s.nb * 4 * n * args.K + s.nb * 2 * n * args.K
@@ -310,6 +315,7 @@ def main_dip(args, ctx):
                 f"K={args.K} dictionary, random-init DIP net per outer iteration)",
         "config": {"workload": (f"LRS-PnP-DIP(pro) {H}x{W}x{B} (BASELINE configs[3]; configs[4] = one such cube per "
                                 f"GPU)" if pro else
+                                f"LRS-PnP-DIP(1-Lip) on a {H}x{W}x{B} cube" if args.cube else
                                 f"LRS-PnP-DIP(1-Lip) on the 200x200x198 cube cropped to {H}x{W}x{B} "
                                 f"(BASELINE configs[2]; 196 = largest 16a-12 size <= 200 that the U-Net maps onto "
                                 f"itself)") + f": {bb}x{bb} blocks ({s.nb}), K={args.K}, Nit={nit} fro4 ISTA + NLM "
@@ -321,10 +327,10 @@ def main_dip(args, ctx):
                                                 f"GEMMs, sigma_max, BN, loss, Adam kernels)",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                     "traffic": load_traffic(f"{tag}_hbm_bytes_per_outer_iter"),
+                     "traffic": load_traffic(f"{tag}_hbm_bytes_per_outer_iter", profiled),
                      "flops_per_outer_iter": flops, "ms_per_outer_iter": dip_ms,
                      "kernels": [ista_entry(f"k_ista_rs (lrs_ista_f32: {s.nb} blocks of {n} rows, Nit {nit})",
-                                            ista_ms, ista_flops, f"{tag}_ista_hbm_bytes_per_launch")]},
+                                            ista_ms, ista_flops, f"{tag}_ista_hbm_bytes_per_launch", profiled)]},
         "mpsnr": {"input": mp0, "after_steps": mp1, "outer_iterations_run": args.warmup + args.steps},
     }
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
