@@ -100,7 +100,7 @@ __device__ __forceinline__ s3f4 s3_mfma6(const s3bf8 (&A)[3], const s3bf8 (&B)[3
 }
 
 // ---- loaders ---------------------------------------------------------------------------------
-// Each provides: static constexpr bool kc; setup(x0, smem) once per workgroup (before the first
+// Each provides: static constexpr bool kc; setup(x0, smem, cls) once per workgroup (before the first
 // barrier); load(x0, k0, kend, v) the thread's 16 values of the step starting at k0 (zero past
 // kend or past the operand's row count).
 
@@ -111,7 +111,7 @@ struct LdDense {
     static constexpr bool pre = false;
     const float *S;
     int ld, X;
-    __device__ __forceinline__ void setup(int, int *) {}
+    __device__ __forceinline__ void setup(int, int *, int) {}
     __device__ __forceinline__ void load(int x0, int k0, int kend, float (&v)[16]) const {
         const int x = x0 + s3_row<KC>(), kb = k0 + s3_kb<KC>();
         if (KC) {
@@ -176,7 +176,8 @@ struct LdPre {
     const __bf16 *P;
     int64_t pstride;
     int ld, X;
-    __device__ __forceinline__ void setup(int, int *) {}
+    int64_t cstride = 0;   // parity-class GEMMs: class cls reads the planes at P + cls * cstride
+    __device__ __forceinline__ void setup(int, int *, int cls) { P += cls * cstride; }
     __device__ __forceinline__ void load(int x0, int k0, int kend, RegP &r) const {
         const int x = x0 + s3_row<true>(), kb = k0 + s3_kb<true>();
         const bool ok = x < X && kb < kend;   // K and kend are multiples of 16
@@ -209,7 +210,7 @@ struct LdFwdTM {
     ConvGeom g;
     int Cp;
     int *tab;
-    __device__ __forceinline__ void setup(int x0, int *smem) {
+    __device__ __forceinline__ void setup(int x0, int *smem, int) {
         tab = smem;
         const int kk = g.k * g.k, P = g.Ho * g.Wo;
         for (int i = threadIdx.x; i < kk * 128; i += blockDim.x) {
@@ -250,7 +251,7 @@ struct LdDgradTM {
     ConvGeom g;
     int Cout, Cop;
     int *tab;
-    __device__ __forceinline__ void setup(int x0, int *smem) {
+    __device__ __forceinline__ void setup(int x0, int *smem, int) {
         tab = smem;
         const int kk = g.k * g.k, Wp = g.Wu + 2 * g.pad, Q = (g.Hu + 2 * g.pad) * Wp;
         for (int i = threadIdx.x; i < kk * 128; i += blockDim.x) {
@@ -292,7 +293,7 @@ struct LdWgradTM {
     ConvGeom g;
     int *tab;   // [2][kk][32]
     int trow, cbase;
-    __device__ __forceinline__ void setup(int x0, int *smem) {
+    __device__ __forceinline__ void setup(int x0, int *smem, int) {
         tab = smem;
         const int r = x0 + s3_row<true>(), kk = g.k * g.k;
         const int c = r / kk, kyx = r - c * kk;
@@ -328,6 +329,198 @@ struct LdWgradTM {
     }
 };
 
+// ---- upsampled 3 x 3 convs by output parity class -------------------------------------------
+// conv3x3(ReflectionPad2d(1)(Upsample2x(x))) (my_Lipschitz_Unet.py:83-94): output pixel
+// (2a + i, 2b + j) reads source rows clamp(a + ey + i - 1), ey in {0, 1}, through the tap sets
+// T(i, ey) = {0} {1, 2} (i = 0) or {0, 1} {2} (i = 1), and likewise the columns: the reflection of the
+// upsampled border is a clamp on the source grid.  Per class the conv is a 2 x 2 conv of x with
+// summed ("effective") weights (k_conv_prep's upc planes): 16 / 9 of the taps of one class, so the
+// four classes cost 4 / 9 of the direct product over the upsampled grid.
+
+__device__ __forceinline__ int clampi(int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
+
+// Forward B of class cls = 2 i + j: col[e * Cp + c][n], n = source pixel (a, b), e = 2 ey + ex:
+// x[c] at (clamp(a + ey + i - 1), clamp(b + ex + j - 1)).  Table [4][128].
+struct LdUpFwdTM {
+    static constexpr bool kc = false;
+    static constexpr bool pre = false;
+    const float *X;
+    int xbytes;
+    ConvGeom g;
+    int Cp;
+    int *tab;
+    __device__ __forceinline__ void setup(int x0, int *smem, int cls) {
+        tab = smem;
+        const int i = cls >> 1, j = cls & 1, Q = g.Hs * g.Ws;
+        for (int idx = threadIdx.x; idx < 4 * 128; idx += blockDim.x) {
+            const int e = idx >> 7, n = x0 + (idx & 127);
+            int o = kOob;
+            if (n < Q) {
+                const int a = n / g.Ws, b = n - a * g.Ws;
+                o = 4 * (clampi(a + (e >> 1) + i - 1, g.Hs) * g.Ws + clampi(b + (e & 1) + j - 1, g.Ws));
+            }
+            tab[idx] = o;
+        }
+    }
+    __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
+        const int r0 = __builtin_amdgcn_readfirstlane(k0 + s3_kb<false>());
+        if (r0 >= kend) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = 0.0f;
+            return;
+        }
+        const int e = r0 / Cp, c0 = r0 - e * Cp;
+        const int pb = g.Hs * g.Ws * 4;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
+        const int vo = tab[e * 128 + s3_row<false>()];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = c0 + u < g.Cin ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
+    }
+};
+
+// Data-gradient B of the same conv over the source grid extended by one pixel on each side
+// (n = (qy + 1)(Ws + 2) + qx + 1, qy in [-1, Hs], qx in [-1, Ws]; k_fold_pad in kPadClamp mode adds
+// the outside ring back onto the border): k = (4 cls + e) Cop + co, dL/dz[co] at
+// (2a + i, 2b + j) with a = qy - ey - i + 1, b = qx - ex - j + 1 when inside.  Table [16][128].
+struct LdUpDgradTM {
+    static constexpr bool kc = false;
+    static constexpr bool pre = false;
+    const float *GY;
+    int gbytes;
+    ConvGeom g;
+    int Cout, Cop;
+    int *tab;
+    __device__ __forceinline__ void setup(int x0, int *smem, int) {
+        tab = smem;
+        const int We = g.Ws + 2, Qe = (g.Hs + 2) * We;
+        for (int idx = threadIdx.x; idx < 16 * 128; idx += blockDim.x) {
+            const int ce = idx >> 7, n = x0 + (idx & 127);
+            int o = kOob;
+            if (n < Qe) {
+                const int qy = n / We - 1, qx = n - (qy + 1) * We - 1, cl = ce >> 2, e = ce & 3;
+                const int i = cl >> 1, j = cl & 1;
+                const int a = qy - (e >> 1) - i + 1, b = qx - (e & 1) - j + 1;
+                if (a >= 0 && a < g.Hs && b >= 0 && b < g.Ws) o = 4 * ((2 * a + i) * g.Wo + 2 * b + j);
+            }
+            tab[idx] = o;
+        }
+    }
+    __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
+        const int r0 = __builtin_amdgcn_readfirstlane(k0 + s3_kb<false>());
+        if (r0 >= kend) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = 0.0f;
+            return;
+        }
+        const int ce = r0 / Cop, c0 = r0 - ce * Cop;
+        const int pb = g.Ho * g.Wo * 4;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(GY, gbytes);
+        const int vo = tab[ce * 128 + s3_row<false>()];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = c0 + u < Cout ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
+    }
+};
+
+// Weight gradient of the same conv by output parity class cls (gridDim.z = 4 classes x split-K):
+// dWE_cls[co][c * 4 + e] = sum over source pixels (a, b) of dL/dz[co] at (2a + i, 2b + j) times x[c]
+// at (clamp(a + ey + i - 1), clamp(b + ex + j - 1)); the classes are stacked in the output
+// ([split][cls][Cout][4 Cin], GemmArgs cls_wo = 0) and k_upc_wgrad_combine sums them into dW.
+// A: dL/dz at the class's output pixels, k = source pixel (16 consecutive per thread).
+struct LdGzCls {
+    static constexpr bool kc = true;
+    static constexpr bool pre = false;
+    const float *GZ;
+    int Hs, Ws, Wo, M;
+    int cls;
+    __device__ __forceinline__ void setup(int, int *, int c) { cls = c; }
+    __device__ __forceinline__ void load(int x0, int k0, int kend, float (&v)[16]) const {
+        const int row = x0 + s3_row<true>(), kb = k0 + s3_kb<true>();
+        const int i = cls >> 1, j = cls & 1;
+        int a = kb / Ws, b = kb - a * Ws;
+        const float *src = GZ + (int64_t)row * (4 * Hs * Ws);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            v[u] = (row < M && kb + u < kend) ? src[(2 * a + i) * Wo + 2 * b + j] : 0.0f;
+            if (++b == Ws) {
+                b = 0;
+                ++a;
+            }
+        }
+    }
+};
+
+// B: col^T of the class, x = r = c * 4 + e, k = source pixel; the step's 32 pixels x 4 taps
+// tabulated one step ahead (double-buffered, as LdWgradTM).
+struct LdWgradCls {
+    static constexpr bool kc = true;
+    static constexpr bool pre = false;
+    const float *X;
+    int xbytes;
+    ConvGeom g;
+    int *tab;   // [2][4][32]
+    int trow, cbase, cls;
+    __device__ __forceinline__ void setup(int x0, int *smem, int c) {
+        tab = smem;
+        cls = c;
+        const int r = x0 + s3_row<true>(), ch = r >> 2, e = r & 3;
+        trow = e * 32 + s3_kb<true>();
+        cbase = ch < g.Cin ? ch * g.Hs * g.Ws * 4 : kOob;
+    }
+    __device__ __forceinline__ void prepare(int k0, int kend, int b) const {
+        const int i = cls >> 1, j = cls & 1;
+        for (int idx = threadIdx.x; idx < 4 * 32; idx += blockDim.x) {
+            const int e = idx >> 5, p = k0 + (idx & 31);
+            int o = kOob;
+            if (p < kend) {
+                const int a = p / g.Ws, bb = p - a * g.Ws;
+                o = 4 * (clampi(a + (e >> 1) + i - 1, g.Hs) * g.Ws + clampi(bb + (e & 1) + j - 1, g.Ws));
+            }
+            tab[b * 4 * 32 + idx] = o;
+        }
+    }
+    __device__ __forceinline__ void load(int, int, int, float (&v)[16], int b) const {
+        const int *t = tab + b * 4 * 32 + trow;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int4 f = *reinterpret_cast<const int4 *>(t + 4 * q);
+            v[4 * q] = s3_bload(rs, f.x + cbase, 0);
+            v[4 * q + 1] = s3_bload(rs, f.y + cbase, 0);
+            v[4 * q + 2] = s3_bload(rs, f.z + cbase, 0);
+            v[4 * q + 3] = s3_bload(rs, f.w + cbase, 0);
+        }
+    }
+};
+
+// dW[co][c][ky][kx] = (sum over the 4 classes of dWE_cls[co][c * 4 + e(cls, ky, kx)], each summed over
+// the nsplit splits in k_gemm_reduce's order) / *div: the chain rule through upc_weight's sums.
+__global__ void k_upc_wgrad_combine(const float *__restrict__ part, int nsplit, int Cout, int Cin,
+                                    const float *div, float *__restrict__ gw) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n = (int64_t)Cout * Cin * 9;
+    if (idx >= n) return;
+    const int tap = (int)(idx % 9), c = (int)((idx / 9) % Cin), co = (int)(idx / (9 * (int64_t)Cin));
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    const int64_t MN = (int64_t)Cout * 4 * Cin;
+    float tot = 0.0f;
+    for (int cl = 0; cl < 4; ++cl) {
+        const int i = cl >> 1, j = cl & 1;
+        const int ey = i == 0 ? (ky == 0 ? 0 : 1) : (ky == 2 ? 1 : 0), ex = j == 0 ? (kx == 0 ? 0 : 1) : (kx == 2 ? 1 : 0);
+        const int64_t off = (int64_t)cl * MN + (int64_t)co * 4 * Cin + c * 4 + 2 * ey + ex;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int z0 = 0; z0 < nsplit; z0 += 8) {
+            float p[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) p[e] = z0 + e < nsplit ? part[(int64_t)(z0 + e) * 4 * MN + off] : 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (z0 + e < nsplit) acc[e] += p[e];
+        }
+        tot = tot + (((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7])));
+    }
+    if (div) tot = tot / *div;
+    gw[idx] = tot;
+}
+
 template <class L>
 struct HasPrepare {
     static constexpr bool value = false;
@@ -335,6 +528,10 @@ struct HasPrepare {
 
 template <>
 struct HasPrepare<LdWgradTM> {
+    static constexpr bool value = true;
+};
+template <>
+struct HasPrepare<LdWgradCls> {
     static constexpr bool value = true;
 };
 
@@ -357,14 +554,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
     const int j = xcd * q8 + min(xcd, r8) + (L >> 3);
     const int bx = j % gridDim.x, byz = j / gridDim.x, by = byz % gridDim.y, bz = byz / gridDim.y;
     const int m0 = by * 128, n0 = bx * 128;
-    const int kbeg = bz * g.kchunk;
+    const int ncls = g.ncls > 1 ? g.ncls : 1, cls = bz % ncls, kz = bz / ncls;   // parity class, split
+    const int kbeg = kz * g.kchunk;
     const int kend = min(g.K, kbeg + g.kchunk);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
     const int jl = lane & 15, gk = lane >> 4;
     constexpr bool PREP = HasPrepare<LB>::value;
-    la.setup(m0, tab);
-    lb.setup(n0, tab);
+    la.setup(m0, tab, cls);
+    lb.setup(n0, tab, cls);
     if constexpr (PREP) lb.prepare(kbeg, kend, 0);
     __syncthreads();
     s3f4 acc[4][4];
@@ -425,9 +623,37 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
             __syncthreads();
         }
     }
-    float *C = g.C + (int64_t)bz * g.M * g.N;
-    const bool final_out = gridDim.z == 1;
+    const int64_t ldc = g.ldc ? g.ldc : g.N;
+    // stacked classes (cls_wo == 0): output [split][cls][M][N]; else the parity scatter below
+    const bool stacked = ncls > 1 && g.cls_wo == 0;
+    float *C = g.C + (int64_t)(stacked ? kz * ncls + cls : kz) * g.M * ldc;
+    const bool final_out = (int)gridDim.z == ncls;
     const float dv = (final_out && g.div) ? *g.div : 1.0f;
+    if (ncls > 1 && !stacked) {
+        // parity class: column n = source pixel (a, b) -> output pixel (2a + i, 2b + j)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int n = n0 + wn + 16 * b + jl;
+            const int sa = n / g.cls_ws, sb = n - sa * g.cls_ws;
+            const int64_t p = (int64_t)(2 * sa + (cls >> 1)) * g.cls_wo + 2 * sb + (cls & 1);
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + wm + 16 * a + 4 * gk + r;
+                    if (m < g.M && n < g.N) {
+                        float v = acc[a][b][r];
+                        if (final_out) {
+                            if (g.bias) v = v + g.bias[m];
+                            if (g.div) v = v / dv;
+                            if (g.accum) v = C[(int64_t)m * ldc + p] + v;
+                        }
+                        C[(int64_t)m * ldc + p] = v;
+                    }
+                }
+        }
+        return;
+    }
     if ((g.N & 3) != 0 || (reinterpret_cast<uintptr_t>(g.C) & 15) != 0) {
         // rows not float4-aligned (odd pixel counts): straight from the MFMA layout, 64-B runs
 #pragma unroll
@@ -657,24 +883,65 @@ __global__ __launch_bounds__(256) void k_pw(PwArgs a) {
 //   WE[p][ci][(ey * ke + ex) * Cop + co] the effective ke x ke kernel of its data gradient as a
 //                                       stride-2 conv over dL/dz (conv_bwd): the sum of the taps
 //                                       W[a + k-1-ey][b + k-1-ex] over the 2 x 2 upsample children a, b
+//   upc: an upsampled reflection-padded 3 x 3 conv run by output parity class (LdUpFwdTM /
+//   LdUpDgradTM): instead of WF / WD,
+//   WUF[p][cls][co][e * Cp + ci]         the class's 2 x 2 effective weights (e = 2 ey + ex, the sum
+//                                        of W[co][ci][ky][kx] over ky in T(i, ey), kx in T(j, ex))
+//   WUD[p][ci][(4 cls + e) * Cop + co]   the same, transposed, all classes (the data gradient's K)
 struct ConvPrep {
     const float *W;
     float *Wn;          // nullable
     __bf16 *wf, *wd;    // nullable (wd holds WE when ke > 0)
     int Cout, Cin, kk, Cp, Cop, si, k, ke;   // si: scale index, -1 = no spectral norm
+    int upc;
 };
+
+// effective weight of parity class (i, j), tap (ey, ex): the taps T(i, ey) x T(j, ex) summed in
+// increasing ky, kx order (w = the 3 x 3 taps of one (co, ci))
+__device__ __forceinline__ float upc_weight(const float *w, int i, int j, int ey, int ex) {
+    const int y0 = (i == 0) ? (ey == 0 ? 0 : 1) : (ey == 0 ? 0 : 2), y1 = (i == 0) ? (ey == 0 ? 0 : 2) : (ey == 0 ? 1 : 2);
+    const int x0 = (j == 0) ? (ex == 0 ? 0 : 1) : (ex == 0 ? 0 : 2), x1 = (j == 0) ? (ex == 0 ? 0 : 2) : (ex == 0 ? 1 : 2);
+    float s = 0.0f;
+    for (int ky = y0; ky <= y1; ++ky)
+        for (int kx = x0; kx <= x1; ++kx) s = s + w[ky * 3 + kx];
+    return s;
+}
 
 __device__ __forceinline__ void conv_prep_body(const ConvPrep &c, float s, int64_t i0, int64_t stride) {
     const int64_t nw = (int64_t)c.Cout * c.Cin * c.kk;
     if (c.Wn)
         for (int64_t i = i0; i < nw; i += stride) c.Wn[i] = c.W[i] / s;
-    const int ed = c.ke > 0 ? c.ke * c.ke : c.kk;
-    const int64_t nf = c.wf ? (int64_t)c.Cout * c.kk * c.Cp : 0, nd = c.wd ? (int64_t)c.Cin * ed * c.Cop : 0;
+    const int ed = c.upc ? 16 : (c.ke > 0 ? c.ke * c.ke : c.kk);
+    const int64_t nf = c.wf ? (int64_t)c.Cout * (c.upc ? 16 : c.kk) * c.Cp : 0, nd = c.wd ? (int64_t)c.Cin * ed * c.Cop : 0;
     for (int64_t i = i0; i < nf + nd; i += stride) {
         float x;
         __bf16 *dst;
         int64_t plane, j;
-        if (i < nf) {
+        if (c.upc) {
+            int cl, e, co, ci;
+            if (i < nf) {   // [cls][co][e * Cp + ci]
+                cl = (int)(i / ((int64_t)c.Cout * 4 * c.Cp));
+                const int rem = (int)(i - (int64_t)cl * c.Cout * 4 * c.Cp);
+                co = rem / (4 * c.Cp);
+                const int r = rem - co * 4 * c.Cp;
+                e = r / c.Cp;
+                ci = r - e * c.Cp;
+                dst = c.wf; plane = nf; j = i;
+            } else {        // [ci][(4 cls + e) * Cop + co]
+                j = i - nf;
+                ci = (int)(j / (16 * c.Cop));
+                const int rem = (int)(j - (int64_t)ci * 16 * c.Cop), ce = rem / c.Cop;
+                co = rem - ce * c.Cop;
+                cl = ce >> 2;
+                e = ce & 3;
+                dst = c.wd; plane = nd;
+            }
+            x = 0.0f;
+            if (co < c.Cout && ci < c.Cin) {
+                x = upc_weight(c.W + ((int64_t)co * c.Cin + ci) * 9, cl >> 1, cl & 1, e >> 1, e & 1);
+                if (c.si >= 0) x = x / s;
+            }
+        } else if (i < nf) {
             const int co = (int)(i / (c.kk * c.Cp)), rem = (int)(i - (int64_t)co * c.kk * c.Cp);
             const int kyx = rem / c.Cp, ci = rem - kyx * c.Cp;
             x = ci < c.Cin ? c.W[((int64_t)co * c.Cin + ci) * c.kk + kyx] : 0.0f;
@@ -825,9 +1092,25 @@ __global__ __launch_bounds__(256) void k_up_border_add(const float *__restrict__
 }
 
 // gx[c][sy][sx] (+)= sum over the x2 upsample children u of sum over the padded positions that
-// read u (direct + reflection mirrors, padded_sources) of gxp[c][iy][ix]
-__global__ __launch_bounds__(256) void k_fold_pad(const float *__restrict__ gxp, ConvGeom gm, float *__restrict__ gx,
-                                                  int accum) {
+// read u (direct + reflection mirrors, padded_sources) of gxp[c][iy][ix], where gxp is the sum of
+// nsplit split-K partials (stride zstride floats; the data-gradient GEMM's split-K finished here, in
+// k_gemm_reduce's order per position)
+__device__ __forceinline__ float fold_term(const float *__restrict__ src, int nsplit, int64_t zstride, int64_t i) {
+    if (nsplit == 1) return src[i];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int z0 = 0; z0 < nsplit; z0 += 8) {
+        float p[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) p[e] = z0 + e < nsplit ? src[(int64_t)(z0 + e) * zstride + i] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (z0 + e < nsplit) acc[e] += p[e];
+    }
+    return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+__global__ __launch_bounds__(256) void k_fold_pad(const float *__restrict__ gxp, int nsplit, int64_t zstride,
+                                                  ConvGeom gm, float *__restrict__ gx, int accum) {
     const int HW = gm.Hs * gm.Ws, Wp = gm.Wu + 2 * gm.pad, Qp = (gm.Hu + 2 * gm.pad) * Wp;
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= HW) return;
@@ -843,7 +1126,7 @@ __global__ __launch_bounds__(256) void k_fold_pad(const float *__restrict__ gxp,
                 int ixs[3];
                 const int nx = padded_sources(gm.up ? 2 * sx + b : sx, gm.Wu, gm.pad, gm.pad_mode, ixs);
                 for (int py = 0; py < ny; ++py)
-                    for (int px = 0; px < nx; ++px) acc += src[iys[py] * Wp + ixs[px]];
+                    for (int px = 0; px < nx; ++px) acc += fold_term(src, nsplit, zstride, iys[py] * Wp + ixs[px]);
             }
         }
         const int64_t i = (int64_t)c * HW + q;

@@ -47,6 +47,11 @@ struct GemmArgs {
     const float *div;    // scalar divisor (device) or null (split == 1 only)
     int M, N, K, kchunk;
     int accum;           // final C += result instead of C = result
+    // k_gemm_s3 only: ncls > 1 output parity classes of an upsampled conv (gridDim.z = ncls x
+    // splits; column n of class cls = 2 i + j is source pixel (a, b) = (n / cls_ws, n % cls_ws),
+    // stored at output pixel (2a + i) cls_wo + 2b + j of rows of ldc floats)
+    int ncls, cls_ws, cls_wo;
+    int64_t ldc;         // output row length (0: N)
 };
 
 // A 128(x) x 16(k) operand tile, 8 values per thread, as two float4 of 4 consecutive k.
@@ -461,12 +466,18 @@ __global__ __launch_bounds__(256) void k_im2col(const float *__restrict__ x, Con
 // Padded positions that read upsampled index u (n = upsampled extent): the direct one and, for
 // reflection, the top/left mirror (u in [1, pad]) and the bottom/right mirror
 // (u in [n-1-pad, n-2]); a tiny extent can have all three.
+// kPadClamp (internal, pad 1 only): the border index also takes the position just outside it --
+// the source-grid form of an upsampled reflection-padded conv (k_gemm_s3's parity classes)
+constexpr int kPadClamp = 2;
 __device__ __forceinline__ int padded_sources(int u, int n, int pad, int mode, int (&iy)[3]) {
     int cnt = 0;
     iy[cnt++] = u + pad;
     if (mode == LRS_PAD_REFLECT && pad > 0) {
         if (u >= 1 && u <= pad) iy[cnt++] = pad - u;
         if (u >= n - 1 - pad && u <= n - 2) iy[cnt++] = 2 * (n - 1) - u + pad;
+    } else if (mode == kPadClamp) {
+        if (u == 0) iy[cnt++] = 0;
+        if (u == n - 1) iy[cnt++] = n + 1;
     }
     return cnt;
 }

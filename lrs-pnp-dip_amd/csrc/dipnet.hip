@@ -163,6 +163,15 @@ inline int r16(int x) { return (x + 15) & ~15; }
 // ~1 % slower than the padded-domain correlation + fold -- the up_4 data-gradient work it saves ran
 // beside that layer's weight gradient anyway, and it adds a split-K reduce and the border launches
 // to the critical chain.  lrs_dip_set_upsample_dgrad(1) selects it (tests cover both).
+// An upsampled, reflection-padded 3 x 3 stride-1 conv runs by output parity class in the network
+// engine (dip_gemm.h LdUpFwdTM / LdUpDgradTM, 4/9 of the direct products).  LRS_DIP_UPC=0 keeps the
+// direct implicit GEMM over the upsampled grid (A/B only).
+inline bool upc_conv(const ConvGeom &g) {
+    static const bool on = !getenv("LRS_DIP_UPC") || atoi(getenv("LRS_DIP_UPC")) != 0;
+    return on && g.up && g.k == 3 && g.pad == 1 && g.pad_mode == LRS_PAD_REFLECT && g.stride == 1 && g.Hs >= 2 &&
+           g.Ws >= 2;
+}
+
 static int g_dip_upeff = 0;
 inline int up_eff_k(const ConvGeom &g) {
     if (!g_dip_upeff || !g.up || g.stride != 1 || g.Hs < 2 || g.Ws < 2) return 0;
@@ -282,9 +291,27 @@ int64_t conv_part_floats(const ConvGeom &g, int Cout) {
     return m;
 }
 
+// split-K scratch of a parity-class conv (network engine only): forward partials over the whole
+// output, the data gradient over the extended source grid, the weight gradient [split][cls][Cout][4 Cin]
+int64_t upc_part_floats(const ConvGeom &g, int Cout) {
+    const int64_t P = (int64_t)g.Ho * g.Wo;
+    int64_t m = 0;
+    const Split f = choose_split(Cout, 4 * g.Hs * g.Ws, 4 * r16(g.Cin), LRS_DIP_SPLIT_BF16, true);
+    if (f.S > 1) m = (int64_t)f.S * Cout * P;
+    m = std::max(m, s3_part_floats(g.Cin, (g.Hs + 2) * (g.Ws + 2), 16 * r16(Cout)));
+    const Split w = choose_split(Cout, 16 * g.Cin, g.Hs * g.Ws, LRS_DIP_SPLIT_BF16, true);
+    return std::max(m, (int64_t)w.S * 16 * Cout * g.Cin);
+}
+
 // bf16 elements of a conv's pre-split weight planes: forward operand WF [3][Cout][kk*Cp], then
 // the data-gradient operand WD [3][Cin][kk*Cop]
-inline int64_t wprep_fwd_elems(const ConvGeom &g, int Cout) { return 3 * (int64_t)Cout * g.k * g.k * r16(g.Cin); }
+// planes of the parity-class forward (WUF) / data gradient (WUD) when upc, else WF / WD (WE)
+inline int64_t wprep_fwd_elems(const ConvGeom &g, int Cout, bool upc = false) {
+    return 3 * (int64_t)Cout * (upc ? 16 : g.k * g.k) * r16(g.Cin);
+}
+inline int64_t wprep_elems(const ConvGeom &g, int Cout, bool upc) {
+    return wprep_fwd_elems(g, Cout, true) + 3 * (int64_t)g.Cin * 16 * r16(Cout);
+}
 inline int64_t wprep_elems(const ConvGeom &g, int Cout) {
     const int ke = up_eff_k(g);
     return wprep_fwd_elems(g, Cout) + 3 * (int64_t)g.Cin * (ke ? ke * ke : g.k * g.k) * r16(Cout);
@@ -310,6 +337,72 @@ int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const 
         hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M, N,
                            bias, div, accum, C);
     }
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+// Forward of an upsampled 3 x 3 conv by output parity class: one launch, gridDim.z = 4 classes x
+// split-K; y (or the split-K partials) over the whole output.  wpre = the WUF planes.
+int upc_fwd(const ConvGeom &g, const float *x, const __bf16 *wpre, const float *bias, int Cout, float *y, float *part,
+            int64_t part_cap, hipStream_t st, int *nsplit_out) {
+    const int Cp = r16(g.Cin), Q = g.Hs * g.Ws, K = 4 * Cp;
+    const int64_t P = (int64_t)g.Ho * g.Wo;
+    const Split s = choose_split(Cout, 4 * Q, K, LRS_DIP_SPLIT_BF16, true);
+    if (nsplit_out) *nsplit_out = s.S;
+    GemmArgs a{nullptr, nullptr, y, bias, nullptr, Cout, Q, K, s.kchunk, 0, 4, g.Ws, g.Wo, P};
+    if (s.S > 1) {
+        if (!part || part_cap < (int64_t)s.S * Cout * P) return LRS_E_WORKSPACE;
+        a.C = part;
+    }
+    const dim3 grid((Q + 127) / 128, (Cout + 127) / 128, 4 * s.S);
+    hipLaunchKernelGGL((k_gemm_s3<LdPre, LdUpFwdTM>), grid, dim3(kGemmThreads), 0, st, a,
+                       LdPre{wpre, (int64_t)4 * Cout * K, K, Cout, (int64_t)Cout * K},
+                       LdUpFwdTM{x, g.Cin * Q * 4, g, Cp, nullptr});
+    if (s.S > 1 && !nsplit_out)
+        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((Cout * P + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S,
+                           Cout, (int)P, bias, nullptr, 0, y);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+// Its data gradient: gxe over the source grid extended by one pixel (one GEMM with K = 4 classes x
+// 4 effective taps x Cout, into the scratch gxe), then k_fold_pad in kPadClamp mode adds the outside
+// ring onto the border pixels (gx += when accum).  wd = the WUD planes.
+int upc_dgrad(const ConvGeom &g, const float *gz, const __bf16 *wd, int Cout, float *gx, float *gxe, float *part,
+              int64_t part_cap, hipStream_t st, int accum) {
+    const int Cop = r16(Cout), K = 16 * Cop, Qe = (g.Hs + 2) * (g.Ws + 2);
+    int nsplit = 1;   // split-K partials are summed inside the fold
+    int rc = gemm_s3_conv(LdPre{wd, (int64_t)g.Cin * K, K, g.Cin}, LdUpDgradTM{gz, Cout * g.Ho * g.Wo * 4, g, Cout, Cop, nullptr},
+                          gxe, nullptr, nullptr, g.Cin, Qe, K, part, part_cap, st, &nsplit);
+    if (rc) return rc;
+    ConvGeom fg = g;
+    fg.up = 0;
+    fg.Hu = g.Hs;
+    fg.Wu = g.Ws;
+    fg.pad = 1;
+    fg.pad_mode = kPadClamp;
+    const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
+    hipLaunchKernelGGL(k_fold_pad, grid, dim3(256), 0, st, nsplit > 1 ? part : gxe, nsplit, (int64_t)g.Cin * Qe, fg, gx,
+                       accum);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+
+// Its weight gradient: per class dWE_cls = dL/dz(class pixels) x col_cls^T (one launch, classes and
+// split-K over gridDim.z, partials [split][cls][Cout][4 Cin] in part), then k_upc_wgrad_combine sums
+// splits and classes into dW (/ *div).
+int upc_wgrad(const ConvGeom &g, const float *gz, const float *x, const float *div, int Cout, float *gw, float *part,
+              int64_t part_cap, hipStream_t st) {
+    const int Q = g.Hs * g.Ws, N = 4 * g.Cin;
+    const Split s = choose_split(Cout, 4 * N, Q, LRS_DIP_SPLIT_BF16, true);
+    if (!part || part_cap < (int64_t)s.S * 4 * Cout * N) return LRS_E_WORKSPACE;
+    const GemmArgs a{nullptr, nullptr, part, nullptr, nullptr, Cout, N, Q, s.kchunk, 0, 4, g.Ws, 0, 0};
+    const dim3 grid((N + 127) / 128, (Cout + 127) / 128, 4 * s.S);
+    hipLaunchKernelGGL((k_gemm_s3<LdGzCls, LdWgradCls>), grid, dim3(kGemmThreads), 0, st, a,
+                       LdGzCls{gz, g.Hs, g.Ws, g.Wo, Cout, 0}, LdWgradCls{x, g.Cin * Q * 4, g, nullptr, 0, 0, 0});
+    const int64_t n = (int64_t)Cout * g.Cin * 9;
+    hipLaunchKernelGGL(k_upc_wgrad_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, s.S, Cout, g.Cin,
+                       div, gw);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -460,12 +553,14 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         // padding / upsample
         const int Cop = r16(Cout);
         const __bf16 *wd = wpre + wprep_fwd_elems(g, Cout);
+        int nsplit = 1;   // split-K partials are summed inside the fold
         rc = gemm_s3_conv(LdPre{wd, (int64_t)g.Cin * kk * Cop, kk * Cop, g.Cin},
                           LdDgradTM{gz, Cout * P * 4, g, Cout, Cop, nullptr}, dcol, nullptr, nullptr, g.Cin, Qp,
-                          kk * Cop, part, part_cap, st);
+                          kk * Cop, part, part_cap, st, &nsplit);
         if (rc) return rc;
         const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
-        hipLaunchKernelGGL(k_fold_pad, grid, dim3(256), 0, st, dcol, g, gx, accum_gx);
+        hipLaunchKernelGGL(k_fold_pad, grid, dim3(256), 0, st, nsplit > 1 ? part : dcol, nsplit, (int64_t)g.Cin * Qp, g,
+                           gx, accum_gx);
         LRS_CHECK_LAUNCH();
         return LRS_OK;
     }
@@ -882,6 +977,7 @@ struct lrs_dipnet {
         int64_t gz_off = -1;          // conv: dL/dz (read by the side-stream weight gradient)
         int sn_index = -1;            // position in the spectral-norm table
         bool sm = false;              // small map: forward / data gradient on k_conv_sm (dip_sm.h)
+        bool upc = false;             // upsampled 3 x 3: forward / data gradient by output parity class
         bool sm_dgrad = false;        // ... data gradient through the adjoint table below
         int64_t adj_off = -1;         // the lists in the workspace (shorts, sm_adj_dim)
         std::vector<int> adj;         // host copy (sm_adj_table), uploaded at bind
@@ -971,7 +1067,10 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
             // a 1x1 conv without BN applies its activation in the pointwise kernel's epilogue
             const bool act_in_pw = !bn && plain_unit(N.g) && wp;
             int nsplit = 1;
-            if (N.sm) {   // small map: implicit GEMM on k_conv_sm, no col written
+            if (N.upc) {   // upsampled 3 x 3: by output parity class
+                rc = upc_fwd(N.g, net->tensor(N.d.in0, x), wp, net->params + N.b_off, N.C, z, net->f(net->part_off),
+                             net->part_cap, st, (fuse || nq) ? &nsplit : nullptr);
+            } else if (N.sm) {   // small map: implicit GEMM on k_conv_sm, no col written
                 const int kk = N.g.k * N.g.k, Cp = r16(N.g.Cin);
                 rc = sm_launch(SmPre{wp, (int64_t)N.C * kk * Cp, kk * Cp, N.C},
                                SmFwd{net->tensor(N.d.in0, x), N.g.Cin * N.g.Hs * N.g.Ws * 4, N.g, Cp, nullptr}, z,
@@ -1128,10 +1227,18 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
                 const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min<int64_t>(N.Kc, 65535));
                 hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, ws, net->tensor(t, x), N.g, net->f(N.col_off));
             }
-            rc = conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, nullptr, net->grads + N.w_off, nullptr,
-                          net->f(net->part2_off), net->part_cap, ws, 0, N.col_off < 0);
+            if (N.upc)
+                rc = upc_wgrad(N.g, gz, net->tensor(t, x), wdiv, N.C, net->grads + N.w_off, net->f(net->part2_off),
+                               net->part_cap, ws);
+            else
+                rc = conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, nullptr, net->grads + N.w_off, nullptr,
+                              net->f(net->part2_off), net->part_cap, ws, 0, N.col_off < 0);
             if (rc) return rc;
-            if (gx && N.sm_dgrad) {   // gx = the adjoint gather of dL/dz on k_conv_sm, one GEMM
+            if (gx && N.upc) {   // by output parity class over the extended source grid, then the clamp fold
+                rc = upc_dgrad(N.g, gz, (const __bf16 *)net->f(N.wpre_off) + wprep_fwd_elems(N.g, N.C, true), N.C, gx,
+                               net->f(net->dcol_off), net->f(net->part_off), net->part_cap, st, written[t]);
+                if (rc) return rc;
+            } else if (gx && N.sm_dgrad) {   // gx = the adjoint gather of dL/dz on k_conv_sm, one GEMM
                 const auto &g = N.g;
                 const int kk = g.k * g.k, Cop = r16(N.C);
                 const __bf16 *wd = (const __bf16 *)net->f(N.wpre_off) + wprep_fwd_elems(g, N.C);
@@ -1278,14 +1385,15 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                         }
                     }
                 } else {
+                    N.upc = upc_conv(N.g);
                     N.wpre_off = ofs;
-                    ofs += align64((wprep_elems(N.g, N.C) + 1) / 2);
+                    ofs += align64(((N.upc ? wprep_elems(N.g, N.C, true) : wprep_elems(N.g, N.C)) + 1) / 2);
                 }
                 if (N.Kc * N.P > max_dcol) max_dcol = N.Kc * N.P;
             }
             if (N.d.bn) { N.z_off = ofs; ofs += align64(N.C * N.P); }
             N.gz_off = ofs; ofs += align64(N.C * N.P);
-            const int64_t pc = conv_part_floats(N.g, N.C);
+            const int64_t pc = std::max(conv_part_floats(N.g, N.C), N.upc ? upc_part_floats(N.g, N.C) : 0);
             if (pc > part) part = pc;
             if (N.C * N.P > max_dz) max_dz = N.C * N.P;
         } else if (N.d.kind == LRS_NODE_BN) {
@@ -1423,10 +1531,10 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
         const auto &N = net->nodes[i];
         if (N.d.kind != LRS_NODE_CONV || (N.sn_index < 0 && N.wpre_off < 0)) continue;
         __bf16 *wf = N.wpre_off >= 0 ? (__bf16 *)net->f(N.wpre_off) : nullptr;
-        __bf16 *wd = (wf && N.d.in0 > 0) ? wf + wprep_fwd_elems(N.g, N.C) : nullptr;
+        __bf16 *wd = (wf && N.d.in0 > 0) ? wf + wprep_fwd_elems(N.g, N.C, N.upc) : nullptr;
         prep.push_back(ConvPrep{params + N.w_off, N.sn_index >= 0 ? net->f(N.wn_off) : nullptr, wf, wd, N.C, N.g.Cin,
                                 N.g.k * N.g.k, r16(N.g.Cin), r16(N.C), N.sn_index, N.g.k,
-                                (wd && !N.sm) ? up_eff_k(N.g) : 0});
+                                (wd && !N.sm && !N.upc) ? up_eff_k(N.g) : 0, N.upc ? 1 : 0});
     }
     hipError_t e = hipSuccess;
     for (const auto &N : net->nodes)
