@@ -85,6 +85,7 @@ def _rand_blocks(rng, nb, n, miss_frac, scale=0.3):
 @pytest.mark.parametrize("bb,nb,Nit,variant,K", [
     (8, 300, 80, "spec2", 256), (8, 129, 100, "fro4", 256), (8, 64, 40, "soft", 256),
     (36, 20, 12, "fro4", 256), (36, 9, 10, "spec2", 256), (8, 70, 30, "matlab", 256), (36, 5, 8, "matlab", 256),
+    (8, 70, 1, "matlab", 256), (36, 5, 1, "matlab", 256),
     # row-split kernel: dictionary sizes other than 256 (main_LRS_PnP.py:159-165 loads a trained
     # dictionary of unknown K), ragged n, many workgroups, every prox
     (36, 40, 10, "fro4", 128), (36, 17, 10, "fro4", 512), (36, 23, 8, "spec2", 200), (36, 30, 6, "soft", 256),
@@ -109,13 +110,21 @@ def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant, K):
     coefs = coefs.cpu().numpy()
     worst = max(rel(coefs[j], Xo[j]) for j in range(nb))
     worst_phi = max(rel(phi[j], PHIo[j]) for j in range(nb))
-    # The MATLAB variant's exp(-d/h^2) weights (no cutoff) amplify the ~1-ulp float32 difference
-    # between the MFMA and the oracle's products: d/h^2 ~ 1e2-1e3 at the reference's h, so the
-    # weights move by ~2 diff dg / h^2 ~ 1e-4 per iteration.  The prox itself is bit-exact
-    # (test_nlm_matlab_prox_bitexact); the iterated coefficients agree to 2e-2 here.
-    tol = 2e-2 if variant == "matlab" else 1e-5
-    assert worst < tol, worst
-    assert worst_phi < tol, worst_phi
+    # The MATLAB variant's exp(-d/h^2) weights (no cutoff) amplify any ~1-ulp float32 difference:
+    # d/h^2 ~ 1e2-1e3 at the reference's h, so the weights move by ~2 diff dg / h^2 ~ 1e-4 per
+    # iteration.  One iteration from identical inputs is held to 1e-5 (the prox itself is bit-exact,
+    # test_nlm_matlab_prox_bitexact); over several iterations the bar is the oracle's own
+    # sensitivity: the oracle re-run on inputs perturbed by 1 float32 ulp, and the kernel may differ
+    # from the oracle by at most 4x that (and 1e-5).
+    tol = 1e-5
+    if variant == "matlab" and Nit > 1:
+        flip = np.where(rng.random(Yb.shape) < 0.5, -1.0, 1.0)
+        Yp = (Yb.astype(np.float64) * (1.0 + flip * 2.0 ** -23)).astype(np.float32)
+        Xp, PHIp = O.ista_batch(Yp, obs, D, alpha, thr, Nit, prox)
+        sens = max(max(rel(Xp[j], Xo[j]) for j in range(nb)), max(rel(PHIp[j], PHIo[j]) for j in range(nb)))
+        tol = max(1e-5, 4.0 * sens)
+    assert worst < tol, (worst, tol)
+    assert worst_phi < tol, (worst_phi, tol)
 
 
 def test_ista_kernel_vs_reference_golden(ops, golden):
