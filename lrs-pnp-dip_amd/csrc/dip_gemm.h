@@ -281,6 +281,36 @@ struct LdDgradTM {
     }
 };
 
+// Lane-per-pixel staging of a weight gradient's col^T tile (128 rows r x 32 pixels per k-step):
+// wave w owns rows 32 w .. 32 w + 31, lane l pixel l & 31 of rows 32 w + 2 u + (l >> 5), u < 16, so
+// each load instruction reads 2 x 32 consecutive pixels of one channel plane (coalesced), and the
+// values go to the row-major LDS image as single bf16 writes.  Rows = (channel, tap) pairs, ntap
+// taps per channel; tab = the step's [ntap][32] source offsets (kOob = zero).
+__device__ __forceinline__ int wlp_row(int u) { return 32 * (threadIdx.x >> 6) + 2 * u + ((threadIdx.x >> 5) & 1); }
+
+__device__ __forceinline__ void wlp_load(const float *X, int xbytes, int plane_bytes, int nrows, int ntap, int x0,
+                                         const int *tab, float (&v)[16]) {
+    const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
+    const int pl = threadIdx.x & 31;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int r = x0 + wlp_row(u), c = r / ntap, tap = r - c * ntap;
+        v[u] = s3_bload(rs, tab[tap * 32 + pl] + (r < nrows ? c * plane_bytes : kOob), 0);
+    }
+}
+
+__device__ __forceinline__ void wlp_store(S3Tile &T, const float (&v)[16]) {
+    const int k = threadIdx.x & 31;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int row = wlp_row(u), at = s3_chunk(row, k >> 3) * 8 + (k & 7);
+        const S3Split q = s3_split(v[u]);
+        T.v[0][row][at] = q.b0;
+        T.v[1][row][at] = q.b1;
+        T.v[2][row][at] = q.b2;
+    }
+}
+
 // Weight-gradient B: col^T, x = r = c * kk + kyx (dW's own column order: a wave's 32 rows are
 // ~4 channels x all taps, whose gathers share cache lines), k = output pixel.  The thread's row
 // is fixed; the step's 32 pixels x kk taps are tabulated one step ahead (prepare,
@@ -288,18 +318,15 @@ struct LdDgradTM {
 struct LdWgradTM {
     static constexpr bool kc = true;
     static constexpr bool pre = false;
+    static constexpr bool lanepix = true;   // wlp_load / wlp_store (coalesced gathers)
     const float *X;
     int xbytes;
     ConvGeom g;
     int *tab;   // [2][kk][32]
-    int trow, cbase;
-    __device__ __forceinline__ void setup(int x0, int *smem, int) {
+    int x0;
+    __device__ __forceinline__ void setup(int x0_, int *smem, int) {
         tab = smem;
-        const int r = x0 + s3_row<true>(), kk = g.k * g.k;
-        const int c = r / kk, kyx = r - c * kk;
-        const bool ok = c < g.Cin;
-        trow = (ok ? kyx : 0) * 32 + s3_kb<true>();
-        cbase = ok ? c * g.Hs * g.Ws * 4 : kOob;
+        x0 = x0_;
     }
     __device__ __forceinline__ void prepare(int k0, int kend, int b) const {
         const int kk = g.k * g.k;
@@ -316,16 +343,7 @@ struct LdWgradTM {
         }
     }
     __device__ __forceinline__ void load(int, int, int, float (&v)[16], int b) const {
-        const int *t = tab + b * 9 * 32 + trow;
-        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int4 f = *reinterpret_cast<const int4 *>(t + 4 * q);
-            v[4 * q] = s3_bload(rs, f.x + cbase, 0);
-            v[4 * q + 1] = s3_bload(rs, f.y + cbase, 0);
-            v[4 * q + 2] = s3_bload(rs, f.z + cbase, 0);
-            v[4 * q + 3] = s3_bload(rs, f.w + cbase, 0);
-        }
+        wlp_load(X, xbytes, g.Hs * g.Ws * 4, g.Cin * g.k * g.k, g.k * g.k, x0, tab + b * 9 * 32, v);
     }
 };
 
@@ -429,22 +447,21 @@ struct LdUpDgradTM {
 struct LdGzCls {
     static constexpr bool kc = true;
     static constexpr bool pre = false;
+    static constexpr bool lanepix = true;   // lane = source pixel (wlp_store), as the col^T side
     const float *GZ;
     int Hs, Ws, Wo, M;
     int cls;
     __device__ __forceinline__ void setup(int, int *, int c) { cls = c; }
     __device__ __forceinline__ void load(int x0, int k0, int kend, float (&v)[16]) const {
-        const int row = x0 + s3_row<true>(), kb = k0 + s3_kb<true>();
-        const int i = cls >> 1, j = cls & 1;
-        int a = kb / Ws, b = kb - a * Ws;
-        const float *src = GZ + (int64_t)row * (4 * Hs * Ws);
+        const int k = k0 + (threadIdx.x & 31), i = cls >> 1, j = cls & 1;
+        const int a = k / Ws, b = k - a * Ws;
+        const int po = (2 * a + i) * Wo + 2 * b + j;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(GZ, M * 4 * Hs * Ws * 4);
+        // the row offset differs between the wave's two halves: in the VGPR offset, not the SGPR one
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            v[u] = (row < M && kb + u < kend) ? src[(2 * a + i) * Wo + 2 * b + j] : 0.0f;
-            if (++b == Ws) {
-                b = 0;
-                ++a;
-            }
+            const int row = x0 + wlp_row(u);
+            v[u] = s3_bload(rs, (k < kend && row < M) ? 4 * po + row * (4 * Hs * Ws * 4) : kOob, 0);
         }
     }
 };
@@ -454,17 +471,16 @@ struct LdGzCls {
 struct LdWgradCls {
     static constexpr bool kc = true;
     static constexpr bool pre = false;
+    static constexpr bool lanepix = true;
     const float *X;
     int xbytes;
     ConvGeom g;
     int *tab;   // [2][4][32]
-    int trow, cbase, cls;
-    __device__ __forceinline__ void setup(int x0, int *smem, int c) {
+    int x0, cls;
+    __device__ __forceinline__ void setup(int x0_, int *smem, int c) {
         tab = smem;
+        x0 = x0_;
         cls = c;
-        const int r = x0 + s3_row<true>(), ch = r >> 2, e = r & 3;
-        trow = e * 32 + s3_kb<true>();
-        cbase = ch < g.Cin ? ch * g.Hs * g.Ws * 4 : kOob;
     }
     __device__ __forceinline__ void prepare(int k0, int kend, int b) const {
         const int i = cls >> 1, j = cls & 1;
@@ -479,16 +495,7 @@ struct LdWgradCls {
         }
     }
     __device__ __forceinline__ void load(int, int, int, float (&v)[16], int b) const {
-        const int *t = tab + b * 4 * 32 + trow;
-        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int4 f = *reinterpret_cast<const int4 *>(t + 4 * q);
-            v[4 * q] = s3_bload(rs, f.x + cbase, 0);
-            v[4 * q + 1] = s3_bload(rs, f.y + cbase, 0);
-            v[4 * q + 2] = s3_bload(rs, f.z + cbase, 0);
-            v[4 * q + 3] = s3_bload(rs, f.w + cbase, 0);
-        }
+        wlp_load(X, xbytes, g.Hs * g.Ws * 4, 4 * g.Cin, 4, x0, tab + b * 4 * 32, v);
     }
 };
 
@@ -524,6 +531,14 @@ __global__ void k_upc_wgrad_combine(const float *__restrict__ part, int nsplit, 
 template <class L>
 struct HasPrepare {
     static constexpr bool value = false;
+};
+template <class L, class = void>
+struct LanePix {
+    static constexpr bool value = false;
+};
+template <class L>
+struct LanePix<L, std::void_t<decltype(L::lanepix)>> {
+    static constexpr bool value = L::lanepix;
 };
 
 template <>
@@ -592,8 +607,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
         int tb = 0;
         for (int k0 = kbeg; k0 < kend; k0 += kS3K) {
             if constexpr (LA::pre) s3_store_pre(As, pa);
+            else if constexpr (LanePix<LA>::value) wlp_store(As, va);
             else s3_store<LA::kc>(As, va);
-            s3_store<LB::kc>(Bs, vb);
+            if constexpr (LanePix<LB>::value) wlp_store(Bs, vb);
+            else s3_store<LB::kc>(Bs, vb);
             if (k0 + kS3K < kend) lb.prepare(k0 + kS3K, kend, tb ^ 1);
             __syncthreads();
             if (k0 + kS3K < kend) {
@@ -611,8 +628,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
         lb.load(n0, kbeg, kend, vb);
         for (int k0 = kbeg; k0 < kend; k0 += kS3K) {
             if constexpr (LA::pre) s3_store_pre(As, pa);
+            else if constexpr (LanePix<LA>::value) wlp_store(As, va);
             else s3_store<LA::kc>(As, va);
-            s3_store<LB::kc>(Bs, vb);
+            if constexpr (LanePix<LB>::value) wlp_store(Bs, vb);
+            else s3_store<LB::kc>(Bs, vb);
             __syncthreads();
             if (k0 + kS3K < kend) {
                 if constexpr (LA::pre) la.load(m0, k0 + kS3K, kend, pa);

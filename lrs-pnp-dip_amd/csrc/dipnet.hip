@@ -399,7 +399,7 @@ int upc_wgrad(const ConvGeom &g, const float *gz, const float *x, const float *d
     const GemmArgs a{nullptr, nullptr, part, nullptr, nullptr, Cout, N, Q, s.kchunk, 0, 4, g.Ws, 0, 0};
     const dim3 grid((N + 127) / 128, (Cout + 127) / 128, 4 * s.S);
     hipLaunchKernelGGL((k_gemm_s3<LdGzCls, LdWgradCls>), grid, dim3(kGemmThreads), 0, st, a,
-                       LdGzCls{gz, g.Hs, g.Ws, g.Wo, Cout, 0}, LdWgradCls{x, g.Cin * Q * 4, g, nullptr, 0, 0, 0});
+                       LdGzCls{gz, g.Hs, g.Ws, g.Wo, Cout, 0}, LdWgradCls{x, g.Cin * Q * 4, g, nullptr, 0, 0});
     const int64_t n = (int64_t)Cout * g.Cin * 9;
     hipLaunchKernelGGL(k_upc_wgrad_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, s.S, Cout, g.Cin,
                        div, gw);
@@ -502,7 +502,7 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         // data gradient only (the weight gradient runs elsewhere)
     } else if (implicit) {
         if (!conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
-        rc = gemm_s3_conv(LdDense<true>{gz, P, Cout}, LdWgradTM{col, g.Cin * g.Hs * g.Ws * 4, g, nullptr, 0, 0}, gw,
+        rc = gemm_s3_conv(LdDense<true>{gz, P, Cout}, LdWgradTM{col, g.Cin * g.Hs * g.Ws * 4, g, nullptr, 0}, gw,
                           nullptr, div, Cout, Kc, P, part, part_cap, st);
     } else {
         // a 1x1 conv's weight gradient (K = all pixels): 128-tiles with deep split-K on the split-bf16
