@@ -1039,6 +1039,12 @@ bool bn_bwd_fusable(const lrs_dipnet *net, int j) {
     return N.d.kind == LRS_NODE_CONV && N.d.bn && N.P <= 4 * kBn1Threads && bn_split(N.P) == 1;
 }
 
+// workgroups per conv of the per-step weight preparation (LRS_DIP_PREP_WG overrides: tuning only)
+inline int prep_blocks() {
+    static const int v = getenv("LRS_DIP_PREP_WG") ? std::max(1, atoi(getenv("LRS_DIP_PREP_WG"))) : 512;
+    return v;
+}
+
 int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_begin = false) {
     int rc;
     if (net->n_sn) {
@@ -1047,7 +1053,7 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
         if (rc) return rc;
     }
     if (net->n_prep) {   // W / scale and the bf16 planes of every conv, one launch
-        hipLaunchKernelGGL(k_conv_prep, dim3(128, net->n_prep), dim3(256), 0, st, net->prep(), net->f(net->scale_off),
+        hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep), dim3(256), 0, st, net->prep(), net->f(net->scale_off),
                            step_begin ? net->loss_acc() : nullptr, net->step());
         LRS_CHECK_LAUNCH();
     }
