@@ -826,7 +826,20 @@ struct BnBwdArgs {
     int lip;                     // BatchNormSpectralNorm rescale (1-Lip) or plain BatchNorm2d
     int accum;                   // gz += instead of gz =
     int vec;                     // float4 path: P, chunk multiples of 4, tensors 16-B aligned
+    const float *beta;           // bn beta_orig: with it the LeakyReLU branch is taken from z (bn_act_bwd)
 };
+
+// dL/d(pre-activation) of a BN node: for LeakyReLU the branch is decided on pre = x_hat gm + bt, the
+// forward's own arithmetic ((z - m) is) gm + bt, so y need not be read (same decisions bitwise: y > 0
+// iff pre > 0); a Sigmoid (or no beta) takes y.
+__device__ __forceinline__ bool bn_needs_y(const BnBwdArgs &a) { return a.act == LRS_ACT_SIGMOID || !a.beta; }
+__device__ __forceinline__ float bn_act_bwd(float g, float xh, float gm, float bt, float y, const BnBwdArgs &a) {
+    if (a.act == LRS_ACT_LRELU && a.beta) {
+        const float pre = xh * gm + bt;
+        return pre > 0.0f ? g : g * 0.2f;
+    }
+    return act_bwd(g, y, a.act);
+}
 
 __device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int sb, double (&o)[3], double *red) {
     const int64_t off = (int64_t)c * a.P;
@@ -1099,6 +1112,9 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__r
     const int c = blockIdx.y, t = threadIdx.x;
     const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
     const float m32 = a.mean[c], is32 = a.invstd[c];
+    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    const float gm = a.gamma[c] / cs, bt = a.beta ? a.beta[c] / cs : 0.0f;
+    const bool ldy = bn_needs_y(a);
     float g[4], xh[4];
     double sg = 0.0, sgx = 0.0, sx = 0.0;
 #pragma unroll
@@ -1116,8 +1132,8 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__r
                 if (z0 + e < nsplit) acc[e] += p[e];
         }
         const float gy = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-        g[u] = act_bwd(gy, a.y[off + i], a.act);
         xh[u] = (a.z[off + i] - m32) * is32;
+        g[u] = bn_act_bwd(gy, xh[u], gm, bt, ldy ? a.y[off + i] : 0.0f, a);
         sg += (double)g[u];
         sgx += (double)g[u] * (double)xh[u];
         sx += (double)xh[u];
@@ -1126,8 +1142,6 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__r
     sg = block_sum_d1(sg, red, par);
     sgx = block_sum_d1(sgx, red, par);
     sx = block_sum_d1(sx, red, par);
-    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
-    const float gm = a.gamma[c] / cs;
     const float k = gm * is32;
     if (t == 0) {
         const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
@@ -1160,6 +1174,9 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd_r(BnBwdArgs a) {
     const float4 *gy4 = reinterpret_cast<const float4 *>(a.gy + off), *y4 = reinterpret_cast<const float4 *>(a.y + off),
                  *z4 = reinterpret_cast<const float4 *>(a.z + off);
     const float m32 = a.mean[c], is32 = a.invstd[c];
+    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    const float gm = a.gamma[c] / cs, bt = a.beta ? a.beta[c] / cs : 0.0f;
+    const bool ldy = bn_needs_y(a);
     float g[NQ][4], xh[NQ][4];
     double sg = 0.0, sgx = 0.0, sx = 0.0;
 #pragma unroll
@@ -1168,12 +1185,12 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd_r(BnBwdArgs a) {
         for (int e = 0; e < 4; ++e) g[u][e] = xh[u][e] = 0.0f;
         if (!bnr_ok<NQ>(a.P, u)) continue;
         const int q = t + u * kBn1Threads;
-        const float4 gv = gy4[q], yv = y4[q], zv = z4[q];
+        const float4 gv = gy4[q], yv = ldy ? y4[q] : make_float4(0.f, 0.f, 0.f, 0.f), zv = z4[q];
         const float ge[4] = {gv.x, gv.y, gv.z, gv.w}, ye[4] = {yv.x, yv.y, yv.z, yv.w}, ze[4] = {zv.x, zv.y, zv.z, zv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            g[u][e] = act_bwd(ge[e], ye[e], a.act);
             xh[u][e] = (ze[e] - m32) * is32;
+            g[u][e] = bn_act_bwd(ge[e], xh[u][e], gm, bt, ye[e], a);
             sg += (double)g[u][e];
             sgx += (double)g[u][e] * (double)xh[u][e];
             sx += (double)xh[u][e];
@@ -1183,8 +1200,6 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd_r(BnBwdArgs a) {
     sg = block_sum_d1(sg, red, par);
     sgx = block_sum_d1(sgx, red, par);
     sx = block_sum_d1(sx, red, par);
-    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
-    const float gm = a.gamma[c] / cs;
     const float k = gm * is32;
     if (t == 0) {
         const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);

@@ -633,13 +633,13 @@ int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, floa
 
 int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, const float *mean,
            const float *invstd, float *gz, float *ggamma, float *gbeta, float *gbias, int C, int64_t P, int act,
-           double *part, hipStream_t st, int lip = 1, int accum = 0) {
+           double *part, hipStream_t st, int lip = 1, int accum = 0, const float *beta = nullptr) {
     const int S = bn_split(P);
     const int vec = (P % 4 == 0 && al16(gy) && al16(y) && al16(z) && al16(gz)) ? 1 : 0;
     int chunk = (int)((P + S - 1) / S);
     if (vec) chunk = (chunk + 3) & ~3;
     BnBwdArgs a{gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, part, C, (int)P, S, chunk,
-                gamma ? 1 : 0, act, lip, accum, vec};
+                gamma ? 1 : 0, act, lip, accum, vec, gamma ? beta : nullptr};
     if (const int nq = gamma ? bn_reg_q(P, vec) : 0) {
         LRS_BNR_SWITCH(nq, k_bn_bwd_r, dim3(1, C), dim3(kBn1Threads), 0, st, a);
     } else if ((gamma || gbias) && S == 1) {
@@ -1204,14 +1204,14 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
             if (pend) {
                 const BnBwdArgs a{nullptr, outp, z, net->params + N.gm_off, net->f(N.mean_off), net->f(N.istd_off), gz,
                                   net->grads + N.gm_off, net->grads + N.bt_off, net->grads + N.b_off, nullptr, N.C,
-                                  (int)N.P, 1, (int)N.P, 1, N.d.act, lip, 0, 0};
+                                  (int)N.P, 1, (int)N.P, 1, N.d.act, lip, 0, 0, net->params + N.bt_off};
                 hipLaunchKernelGGL(k_reduce_bn_bwd1, dim3(1, N.C), dim3(kBn1Threads), 0, st, pend, pend_S, a);
                 pend = nullptr;
             } else if (!(head_done && i == n - 1)) {   // else k_mse_head wrote gz and the bias gradient
                 rc = bn_bwd(gout, outp, z, bn ? net->params + N.gm_off : nullptr, net->f(N.mean_off),
                             net->f(N.istd_off), gz, bn ? net->grads + N.gm_off : nullptr,
                             bn ? net->grads + N.bt_off : nullptr, net->grads + N.b_off, N.C, N.P, N.d.act,
-                            net->bnpart(), st, lip, 0);
+                            net->bnpart(), st, lip, 0, bn ? net->params + N.bt_off : nullptr);
                 if (rc) return rc;
             }
             const int t = N.d.in0;
