@@ -1431,28 +1431,27 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     const SnConv cv = convs[blockIdx.x];
     const int m = cv.rows <= cv.cols ? cv.rows : cv.cols;
     const double *G = gram + (int64_t)blockIdx.x * kSnGramDoubles;
-    extern __shared__ double Gs[];                // [kSnMaxDim][kSnMaxDim + 1] (dynamic, 129 KB)
     __shared__ __attribute__((aligned(16))) double q[kSnMaxDim];
     __shared__ __attribute__((aligned(16))) double2 ab[kSnMaxDim];   // {alpha_i, beta_{i-1}^2}
     __shared__ int best_s[3];
     const int t = threadIdx.x, row = t >> 1, half = t & 1;
     if (t < 3) best_s[t] = -1;
-    // the reduced Gram (k_sn_gram_reduce): 16-B loads, all in flight
+    // the thread's half row of the reduced Gram (k_sn_gram_reduce), straight into registers: 32
+    // contiguous 16-B loads, all in flight.  (No LDS staging: a kernel that asked for the 129 KB a
+    // staged copy needs could not start on any CU that held a sparse-coding workgroup, so the DIP
+    // stalled at every step's sigma while the sparse coding ran beside it.)
+    double g[64];
     {
+        const double2 *src = reinterpret_cast<const double2 *>(G + (int64_t)row * kSnMaxDim + half * 64);
         double2 pv[32];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) pv[u] = *reinterpret_cast<const double2 *>(G + 2 * (t + 256 * u));
+        for (int u = 0; u < 32; ++u) pv[u] = src[u];
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
-            const int e = 2 * (t + 256 * u), r = e / kSnMaxDim, c = e % kSnMaxDim;
-            Gs[r * (kSnMaxDim + 1) + c] = pv[u].x;
-            Gs[r * (kSnMaxDim + 1) + c + 1] = pv[u].y;
+            g[2 * u] = pv[u].x;
+            g[2 * u + 1] = pv[u].y;
         }
     }
-    __syncthreads();
-    double g[64];
-#pragma unroll
-    for (int c = 0; c < 64; ++c) g[c] = Gs[row * (kSnMaxDim + 1) + half * 64 + c];
     if (prof && t == 0) prof[blockIdx.x * 8 + 1] = wall_clock64();
     int par = 0, rnd = 0;
     // Lanczos on the unnormalised residual r_k (r_0 = start vector): one matvec u' = G r_k, one

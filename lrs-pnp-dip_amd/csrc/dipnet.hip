@@ -656,10 +656,7 @@ int sn_launch(const SnConv *table_dev, int n, int64_t max_elems, double *gram, f
               float ln_lambda, bool apply, hipStream_t st, long long *prof = nullptr) {
     hipLaunchKernelGGL(k_sn_gram, dim3(kSnSplit, n), dim3(256), 0, st, table_dev, gram);
     hipLaunchKernelGGL(k_sn_gram_reduce, dim3(kSnPairs, n), dim3(256), 0, st, table_dev, gram);
-    const size_t lds = sizeof(double) * kSnMaxDim * (kSnMaxDim + 1);
-    hipError_t e = hipFuncSetAttribute((const void *)k_sn_sigma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_sn_sigma, dim3(n), dim3(256), lds, st, table_dev, gram, sigma, scale, ln_lambda, prof);
+    hipLaunchKernelGGL(k_sn_sigma, dim3(n), dim3(256), 0, st, table_dev, gram, sigma, scale, ln_lambda, prof);
     if (apply) hipLaunchKernelGGL(k_sn_apply, dim3(ew_blocks(max_elems, 256), n), dim3(kEw), 0, st, table_dev, scale);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
