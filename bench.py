@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="process group: nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU)")
+                    help="process group: nccl (= RCCL, one GPU per rank) or gloo (rehearsal: rank r on GPU "
+                         "r mod the visible count, so ranks share cuda:0 on a 1-GPU box)")
     ap.add_argument("--split-cube", action="store_true",
                     help="one cube over all ranks (strong scaling): pnp in pixel-row slabs; dip task-parallel "
                          "(DIP on rank 0, sparse coding over the others)")

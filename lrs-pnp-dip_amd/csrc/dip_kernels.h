@@ -1390,11 +1390,24 @@ __device__ int sturm_gt(const double2 *ab, int n, double x) {
 // round, before its barrier, and last read two rounds ago.  One barrier per round.
 __device__ __forceinline__ double sn_grid(double base, double step, int t) { return base + step * (double)(t + 1); }
 
+// max over the 64 lanes (uniform): DPP row steps, then the four rows' values by readlane
+__device__ __forceinline__ int wave_max_i(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));   // row_mirror
+    return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
 __device__ __forceinline__ int sn_round(const double2 *ab, int n, double base, double step, int *best, int &rnd) {
     const int t = threadIdx.x;
     int *slot = best + rnd % 3;
     if (t == 0) best[(rnd + 1) % 3] = -1;
-    if (sturm_gt(ab, n, sn_grid(base, step, t)) >= 1) atomicMax(slot, t);
+    // the wave's largest flagged t by DPP, then one LDS atomic per wave (a per-lane atomicMax
+    // compiled to a scalar loop over the flagged lanes)
+    const int wmax = wave_max_i(sturm_gt(ab, n, sn_grid(base, step, t)) >= 1 ? t : -1);
+    if ((t & 63) == 0 && wmax >= 0) atomicMax(slot, wmax);
     __syncthreads();
     const int bt = *slot;
     ++rnd;
@@ -1434,18 +1447,28 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     __shared__ __attribute__((aligned(16))) double q[kSnMaxDim];
     __shared__ __attribute__((aligned(16))) double2 ab[kSnMaxDim];   // {alpha_i, beta_{i-1}^2}
     __shared__ int best_s[3];
-    const int t = threadIdx.x, row = t >> 1, half = t & 1;
+    // Matvec blocking: thread t holds the 4 x 16 block of G at rows 4 rb .. 4 rb + 3 (rb = t >> 3),
+    // columns 16 cb .. 16 cb + 15 (cb = t & 7), so a step reads 16 values of q from LDS per thread
+    // (a quarter of what half rows needed: the LDS return bandwidth was the step's largest cost),
+    // and the 8 lanes of a row block sum their partials by DPP.  Vector entries: row = 4 rb +
+    // (cb & 3), held by lanes cb and cb + 4 (half = cb >> 2; half 0 contributes and writes q).
+    // Column chunk c (2 doubles) of a thread is 2 ((c + cb) & 7): the 8 lanes of a row block read
+    // distinct LDS banks.
+    const int t = threadIdx.x, rb = t >> 3, cb = t & 7, row = 4 * rb + (cb & 3), half = cb >> 2;
     if (t < 3) best_s[t] = -1;
-    // the thread's half row of the reduced Gram (k_sn_gram_reduce), straight into registers: 32
-    // contiguous 16-B loads, all in flight.  (No LDS staging: a kernel that asked for the 129 KB a
-    // staged copy needs could not start on any CU that held a sparse-coding workgroup, so the DIP
+    // the thread's block of the reduced Gram (k_sn_gram_reduce), straight into registers: 32
+    // 16-B loads, all in flight.  (No LDS staging: a kernel that asked for the 129 KB a staged
+    // copy needs could not start on any CU that held a sparse-coding workgroup, so the DIP
     // stalled at every step's sigma while the sparse coding ran beside it.)
-    double g[64];
+    double g[64];   // g[16 i + 2 c + e] = G[4 rb + i][16 cb + 2 ((c + cb) & 7) + e]
     {
-        const double2 *src = reinterpret_cast<const double2 *>(G + (int64_t)row * kSnMaxDim + half * 64);
         double2 pv[32];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) pv[u] = src[u];
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                pv[8 * i + c] = *reinterpret_cast<const double2 *>(G + (int64_t)(4 * rb + i) * kSnMaxDim + 16 * cb +
+                                                                   2 * ((c + cb) & 7));
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
             g[2 * u] = pv[u].x;
@@ -1472,22 +1495,36 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
     int k = 0;
     long long tcheck = 0, ccheck = 0;
     for (; k < m; ++k) {
-        // all 32 b128 reads of this thread's half of q are issued before the first FMA (left to
-        // itself the compiler waited on each read: ~2.5 us per step instead of ~0.5)
-        double qv[64];
-        const double2 *q2 = reinterpret_cast<const double2 *>(q + half * 64);
+        // all 8 b128 reads of this thread's 16 entries of q are issued before the first FMA (left
+        // to itself the compiler waited on each read)
+        double qv[16];
 #pragma unroll
-        for (int c = 0; c < 32; ++c) {
-            const double2 v = q2[c];
+        for (int c = 0; c < 8; ++c) {
+            const double2 v = *reinterpret_cast<const double2 *>(q + 16 * cb + 2 * ((c + cb) & 7));
             qv[2 * c] = v.x;
             qv[2 * c + 1] = v.y;
         }
         __builtin_amdgcn_sched_barrier(0);
-        double acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};    // 8 independent FMA chains
+        double u4[4];
 #pragma unroll
-        for (int c = 0; c < 64; ++c) acc8[c & 7] = __fma_rn(g[c], qv[c], acc8[c & 7]);
-        double u = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
-        u += __shfl_xor(u, 1, 64);
+        for (int i = 0; i < 4; ++i) {   // two independent FMA chains per row
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 16; c += 2) {
+                s0 = __fma_rn(g[16 * i + c], qv[c], s0);
+                s1 = __fma_rn(g[16 * i + c + 1], qv[c + 1], s1);
+            }
+            u4[i] = s0 + s1;
+        }
+        // sum over the row block's 8 lanes (xor 1, xor 2, then lane i + lane 7 - i)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            u4[i] += dpp_d<0xB1>(u4[i]);
+            u4[i] += dpp_d<0x4E>(u4[i]);
+            u4[i] += dpp_d<0x141>(u4[i]);
+        }
+        const int own = cb & 3;
+        double u = own == 0 ? u4[0] : own == 1 ? u4[1] : own == 2 ? u4[2] : u4[3];
         const double w_rr = wave_sum_d(half == 0 ? rr * rr : 0.0);
         const double w_ru = wave_sum_d(half == 0 ? rr * u : 0.0);
         if ((t & 63) == 0) {

@@ -37,6 +37,10 @@ def init_from_env(backend: str = "nccl") -> Ctx:
     if backend == "nccl":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
+    elif torch.cuda.is_available():
+        # gloo rehearsal: ranks spread over the visible GPUs (LOCAL_RANK mod count), so on a
+        # 1-GPU box they share cuda:0 and on a multi-GPU node each rank still gets its own card
+        torch.cuda.set_device(local % torch.cuda.device_count())
     if world > 1 and not dist.is_initialized():
         kw = {"device_id": dev} if (backend == "nccl" and dev is not None) else {}
         dist.init_process_group(backend, **kw)
