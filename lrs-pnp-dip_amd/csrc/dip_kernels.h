@@ -1346,8 +1346,7 @@ __global__ __launch_bounds__(256) void k_sn_gram_reduce(const SnConv *convs, dou
 // number of eigenvalues of the symmetric tridiagonal T_n above x, T_n given as ab[i] = {alpha_i,
 // beta_{i-1}^2}: n minus the sign changes of the characteristic-polynomial sequence p_i =
 // (alpha_i - x) p_{i-1} - beta_{i-1}^2 p_{i-2} (division-free; rescaled by a power of two every 4
-// terms, which changes no sign).  The next four terms' LDS reads are in flight while four are
-// evaluated.
+// terms, which changes no sign).
 __device__ __forceinline__ void sturm_term(double a, double b2, double x, double &p, double &pm, int &changes) {
     double pn = __fma_rn(a - x, p, -b2 * pm);
     // a zero takes the sign opposite to its predecessor: perturb it to -p * 2^-600 (the usual
@@ -1358,7 +1357,7 @@ __device__ __forceinline__ void sturm_term(double a, double b2, double x, double
     p = pn;
 }
 
-__device__ int sturm_gt(const double2 *ab, int n, double x) {
+__device__ __noinline__ int sturm_gt_checked(const double2 *ab, int n, double x) {
     double pm = 1.0, p = ab[0].x - x;
     p = p != 0.0 ? p : -0x1p-600;              // p_0 = 1 > 0: a zero p_1 counts as negative
     int changes = p < 0.0;
@@ -1381,6 +1380,50 @@ __device__ int sturm_gt(const double2 *ab, int n, double x) {
     }
     for (; i < n; ++i) sturm_term(ab[i].x, ab[i].y, x, p, pm, changes);
     return n - changes;
+}
+
+// The same count with the zero test off the recurrence's dependency chain: the terms are
+// evaluated unperturbed and any exact zero is only recorded; a sequence that met one (rare) is
+// re-evaluated by sturm_gt_checked.  Without a zero both evaluate the same values (the power-of-
+// two rescaling, here every 8 terms, is exact), so the count is the checked one.  Eight terms'
+// LDS reads are in flight while eight are evaluated.
+__device__ __forceinline__ int sturm_gt(const double2 *ab, int n, double x) {
+    double pm = 1.0, p = ab[0].x - x;
+    if (p == 0.0) return sturm_gt_checked(ab, n, x);
+    int changes = p < 0.0;
+    bool zero = false;
+    int i = 1;
+    double2 c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = ab[min(i + j, kSnMaxDim - 1)];
+    for (; i + 8 <= n; i += 8) {
+        double2 nx[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nx[j] = ab[min(i + 8 + j, kSnMaxDim - 1)];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const double pn = __fma_rn(c[j].x - x, p, -c[j].y * pm);
+            zero |= pn == 0.0;
+            changes += (int)((unsigned long long)(__double_as_longlong(pn) ^ __double_as_longlong(p)) >> 63);
+            pm = p;
+            p = pn;
+        }
+        int e;
+        frexp(fabs(p) > fabs(pm) ? p : pm, &e);
+        p = ldexp(p, -e);
+        pm = ldexp(pm, -e);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c[j] = nx[j];
+    }
+    for (; i < n; ++i) {
+        const double pn = __fma_rn(ab[i].x - x, p, -ab[i].y * pm);
+        zero |= pn == 0.0;
+        changes += (int)((unsigned long long)(__double_as_longlong(pn) ^ __double_as_longlong(p)) >> 63);
+        pm = p;
+        p = pn;
+    }
+    return zero ? sturm_gt_checked(ab, n, x) : n - changes;
 }
 
 // One 256-point multisection round on T_n: thread t tests x_t = base + step (t + 1); returns (to
