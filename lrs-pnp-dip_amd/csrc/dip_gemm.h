@@ -763,13 +763,17 @@ inline int pw_ldsrow(int Kp32) {   // bytes; Kp32 * 2 rounded up to 16 mod 256
     return b + (((16 - b) % 256) + 256) % 256;
 }
 
-template <int MT>
-__global__ __launch_bounds__(256) void k_pw(PwArgs a) {
+// NB = 16-pixel column blocks per workgroup (16 NB pixels): 4, or 5 where 16 x 5 = 80 pixels per
+// workgroup bring the grid under one round of the CUs' workgroup slots (the 198-row last 1x1 at
+// 196^2: 481 workgroups at 2 per CU instead of 600).
+template <int MT, int NB = 4>
+__global__ __launch_bounds__(256, 2) void k_pw(PwArgs a) {
     extern __shared__ __attribute__((aligned(16))) char pw_smem[];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, jl = lane & 15, gk = lane >> 4;
-    const int64_t n0 = (int64_t)blockIdx.x * 64;
-    const int64_t plane = (int64_t)64 * a.ldsrow;
-    {   // stage: thread (n = t & 63) splits k chunks (t >> 6) + 4 i of 8 values each.  Buffer
+    constexpr int NPX = 16 * NB;
+    const int64_t n0 = (int64_t)blockIdx.x * NPX;
+    const int64_t plane = (int64_t)NPX * a.ldsrow;
+    if constexpr (NB == 4) {   // stage: thread (n = t & 63) splits k chunks (t >> 6) + 4 i of 8 values each.  Buffer
         // loads, branch-free: k (wave-uniform) goes in the scalar offset, so rows k >= K fall past
         // the buffer's K * N floats and read 0; a pixel n >= N reads at kOob.
         const int n = t & 63;
@@ -803,12 +807,44 @@ __global__ __launch_bounds__(256) void k_pw(PwArgs a) {
             *reinterpret_cast<s3bf8 *>(dst + plane) = p1;
             *reinterpret_cast<s3bf8 *>(dst + 2 * plane) = p2;
         }
+    } else {   // NPX pixels x nck chunks as items it = t + 256 j: pixel it % NPX, chunk it / NPX
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(a.B, (int)(a.K * a.N * 4));
+        const int nck = a.Kp32 / 8, items = NPX * nck;
+        constexpr int kMaxIt = (NPX * 32 + 255) / 256;   // K <= 256
+        float v[kMaxIt][8];
+#pragma unroll
+        for (int j = 0; j < kMaxIt; ++j) {
+            const int it = t + 256 * j, n = it % NPX, c = it / NPX;
+            const int voff = n0 + n < a.N ? (int)((n0 + n) * 4) : kOob;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t so = (int64_t)(8 * c + u) * a.N * 4;
+                v[j][u] = (it < items && !(a.dbg & 4)) ? s3_bload(rs, voff, so < kOob ? (int)so : kOob) : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kMaxIt; ++j) {
+            const int it = t + 256 * j, n = it % NPX, c = it / NPX;
+            if (it >= items) break;
+            s3bf8 p0, p1, p2;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const S3Split q = s3_split(v[j][u]);
+                p0[u] = q.b0;
+                p1[u] = q.b1;
+                p2[u] = q.b2;
+            }
+            char *dst = pw_smem + (int64_t)n * a.ldsrow + 16 * c;
+            *reinterpret_cast<s3bf8 *>(dst) = p0;
+            *reinterpret_cast<s3bf8 *>(dst + plane) = p1;
+            *reinterpret_cast<s3bf8 *>(dst + 2 * plane) = p2;
+        }
     }
-    s3f4 acc[MT][4];
+    s3f4 acc[MT][NB];
 #pragma unroll
     for (int j = 0; j < MT; ++j)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[j][b] = s3f4{0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < NB; ++b) acc[j][b] = s3f4{0.f, 0.f, 0.f, 0.f};
     const int ksteps = a.Kp32 / 32;
     s3bf8 fa[MT][3], fn[MT][3];
     // A fragments: 16-B buffer loads (L2-resident planes), rows >= M and k >= lda at kOob (zeros)
@@ -824,13 +860,20 @@ __global__ __launch_bounds__(256) void k_pw(PwArgs a) {
                 f[j][p] = __builtin_bit_cast(s3bf8, __builtin_amdgcn_raw_buffer_load_b128(ra, vo, (int)(2 * p * a.pstride), 0));
         }
     };
+    // NB = 4 prefetches the next k-step's A fragments; NB = 5 has no registers for that (its loads
+    // overlap the step's B fragment reads from LDS instead)
+    constexpr bool PF = NB == 4;
     loadA(0, fa);
     __syncthreads();
     for (int ks = 0; ks < ksteps; ++ks) {
-        if (ks + 1 < ksteps) loadA(ks + 1, fn);
-        s3bf8 fb[4][3];
+        if constexpr (PF) {
+            if (ks + 1 < ksteps) loadA(ks + 1, fn);
+        } else if (ks > 0) {
+            loadA(ks, fa);
+        }
+        s3bf8 fb[NB][3];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < NB; ++b) {
             const char *s0 = pw_smem + (int64_t)(16 * b + jl) * a.ldsrow + 16 * (4 * ks + gk);
 #pragma unroll
             for (int p = 0; p < 3; ++p) fb[b][p] = *reinterpret_cast<const s3bf8 *>(s0 + p * plane);
@@ -838,8 +881,8 @@ __global__ __launch_bounds__(256) void k_pw(PwArgs a) {
 #pragma unroll
         for (int j = 0; j < MT; ++j)
 #pragma unroll
-            for (int b = 0; b < 4; ++b) acc[j][b] = s3_mfma6(fa[j], fb[b], acc[j][b]);
-        if (ks + 1 < ksteps) {
+            for (int b = 0; b < NB; ++b) acc[j][b] = s3_mfma6(fa[j], fb[b], acc[j][b]);
+        if (PF && ks + 1 < ksteps) {
 #pragma unroll
             for (int j = 0; j < MT; ++j)
 #pragma unroll
@@ -850,23 +893,24 @@ __global__ __launch_bounds__(256) void k_pw(PwArgs a) {
     // of each row block as [row][pixel] and reads it back as float4 rows, so every 16 lanes store
     // one full 256-B pixel run of a channel row (the MFMA layout gives a lane 4 rows of 1 pixel)
     __syncthreads();
-    float *E = reinterpret_cast<float *>(pw_smem) + wv * 16 * 68;
+    constexpr int ES = NPX + 4;   // staging row stride (floats)
+    float *E = reinterpret_cast<float *>(pw_smem) + wv * 16 * ES;
     const bool vec = (a.N & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.C) & 15) == 0);
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < NB; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) E[(4 * gk + r) * 68 + 16 * b + jl] = acc[j][b][r];
+            for (int r = 0; r < 4; ++r) E[(4 * gk + r) * ES + 16 * b + jl] = acc[j][b][r];
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done (wave-local tile)
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int idx = lane + 64 * i, rr = idx >> 4, q = 4 * (idx & 15);
+        for (int i = 0; i < NB; ++i) {   // 16 rows x NPX / 4 float4 runs
+            const int idx = lane + 64 * i, rr = idx / (4 * NB), q = 4 * (idx % (4 * NB));
             const int m = 16 * wv + 64 * j + rr;
             const int64_t n = n0 + q;
             if (m >= a.M || (a.dbg & 1)) continue;
-            float4 v = *reinterpret_cast<const float4 *>(E + rr * 68 + q);
+            float4 v = *reinterpret_cast<const float4 *>(E + rr * ES + q);
             const float bs = a.bias ? a.bias[m] : 0.0f;
             float *c = a.C + (int64_t)m * a.N + n;
             if (vec && n + 3 < a.N) {

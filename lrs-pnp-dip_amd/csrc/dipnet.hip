@@ -429,32 +429,47 @@ void wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, 
     hipLaunchKernelGGL(k_conv_prep1, dim3(ew_blocks(n, 2048)), dim3(256), 0, st, c);
 }
 
+// LRS_DIP_PW_WIDE=0 keeps 64-pixel workgroups for M > 192 (A/B only)
+inline bool pw_wide() {
+    static const bool v = !getenv("LRS_DIP_PW_WIDE") || atoi(getenv("LRS_DIP_PW_WIDE")) != 0;
+    return v;
+}
+
 // Pointwise conv product on k_pw (A: pre-split planes [3][M][lda], B: [K][N] fp32).
 int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, int K, int64_t N, float *C,
               const float *bias, int accum, hipStream_t st, int act = 0) {
     if (M <= 0 || N <= 0) return LRS_OK;
     if (M > 256 || lda < K || lda % 16) return LRS_E_UNSUPPORTED;
     const int Kp32 = (int)round_up(lda, 32), ldsrow = pw_ldsrow(Kp32);
-    const int lds = 3 * 64 * ldsrow;
+    // four row blocks (M > 192): 80-pixel workgroups (k_pw<4, 5>), whose grid fits one round of
+    // the 2-per-CU slots that kernel's registers allow where 64-pixel ones need 1.2 rounds
+    const bool wide = (M + 63) / 64 == 4 && pw_wide();
+    const int npx = wide ? 80 : 64;
+    const int lds = 3 * npx * ldsrow;
     static bool attr_set = false;
-    if (!attr_set) {   // up to K = 256: 3 x 64 x 528 B
+    if (!attr_set) {   // up to K = 256: 3 x 64 (80) x 528 B
         const int mx = 3 * 64 * pw_ldsrow(256);
         hipError_t e = hipFuncSetAttribute((const void *)k_pw<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
         if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
         if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
         if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<4>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void *)k_pw<4, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * 80 * pw_ldsrow(256));
         if (e != hipSuccess) return (int)e;
         attr_set = true;
     }
     if (Kp32 > 256 || (int64_t)K * N * 4 >= kOob || 3 * pstride * 2 >= kOob) return LRS_E_UNSUPPORTED;
     static const int dbg = getenv("LRS_PW_DBG") ? atoi(getenv("LRS_PW_DBG")) : 0;
     const PwArgs a{A, pstride, lda, B, K, N, C, bias, M, Kp32, ldsrow, accum, dbg, act};
-    const dim3 grid((unsigned)((N + 63) / 64));
+    const dim3 grid((unsigned)((N + npx - 1) / npx));
     switch ((M + 63) / 64) {
     case 1: hipLaunchKernelGGL(k_pw<1>, grid, dim3(256), lds, st, a); break;
     case 2: hipLaunchKernelGGL(k_pw<2>, grid, dim3(256), lds, st, a); break;
     case 3: hipLaunchKernelGGL(k_pw<3>, grid, dim3(256), lds, st, a); break;
-    default: hipLaunchKernelGGL(k_pw<4>, grid, dim3(256), lds, st, a); break;
+    default:
+        if (wide) hipLaunchKernelGGL((k_pw<4, 5>), grid, dim3(256), lds, st, a);
+        else hipLaunchKernelGGL(k_pw<4>, grid, dim3(256), lds, st, a);
+        break;
     }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
