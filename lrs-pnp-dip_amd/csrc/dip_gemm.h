@@ -763,9 +763,8 @@ inline int pw_ldsrow(int Kp32) {   // bytes; Kp32 * 2 rounded up to 16 mod 256
     return b + (((16 - b) % 256) + 256) % 256;
 }
 
-// NB = 16-pixel column blocks per workgroup (16 NB pixels): 4, or 5 where 16 x 5 = 80 pixels per
-// workgroup bring the grid under one round of the CUs' workgroup slots (the 198-row last 1x1 at
-// 196^2: 481 workgroups at 2 per CU instead of 600).
+// NB = 16-pixel column blocks per workgroup (16 NB pixels): 4, or 5, chosen per launch by
+// pw_launch (dipnet.hip) from the rounds of CU slots the grid needs.
 template <int MT, int NB = 4>
 __global__ __launch_bounds__(256, 2) void k_pw(PwArgs a) {
     extern __shared__ __attribute__((aligned(16))) char pw_smem[];

@@ -429,48 +429,65 @@ void wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, 
     hipLaunchKernelGGL(k_conv_prep1, dim3(ew_blocks(n, 2048)), dim3(256), 0, st, c);
 }
 
-// LRS_DIP_PW_WIDE=0 keeps 64-pixel workgroups for M > 192 (A/B only)
-inline bool pw_wide() {
-    static const bool v = !getenv("LRS_DIP_PW_WIDE") || atoi(getenv("LRS_DIP_PW_WIDE")) != 0;
-    return v;
+// LRS_DIP_PW_NB = the allowed NB digits, e.g. "4" keeps 64-pixel workgroups everywhere (A/B only)
+inline bool pw_nb_allowed(int nb) {
+    static const char *v = getenv("LRS_DIP_PW_NB");
+    return !v || strchr(v, '0' + nb) != nullptr;
 }
 
+// k_pw instantiations: MT row blocks x NB 16-pixel column blocks, and the workgroups per CU their
+// registers allow (one wave per SIMD each; gfx950: 512 VGPRs per SIMD lane over the waves, in
+// granules of 8; the counts of the current build: 80, 150, 192, 234, 198).  48-pixel workgroups
+// (NB = 3) for the LDS-bound K = 198 data gradient measured ~10 us per 196^2 step slower (A/B,
+// LRS_DIP_PW_NB) and were dropped.
+struct PwKernel {
+    int mt, nb, wg_per_cu;
+    void (*fn)(PwArgs);
+};
+static const PwKernel kPwKernels[] = {
+    {1, 4, 6, k_pw<1, 4>}, {2, 4, 3, k_pw<2, 4>}, {3, 4, 2, k_pw<3, 4>}, {4, 4, 2, k_pw<4, 4>}, {4, 5, 2, k_pw<4, 5>},
+};
+
 // Pointwise conv product on k_pw (A: pre-split planes [3][M][lda], B: [K][N] fp32).
+// The pixel width of a workgroup is chosen per launch: the fewest rounds of the CU slots (LDS
+// 3 x 16 NB x ldsrow bytes and the registers both limit them) times the per-workgroup work (NB),
+// wider on ties.  At 196^2 the 198-row last 1x1 runs on 80 pixels: 481 workgroups, one round of
+// 2 per CU instead of 1.2 rounds at 64 (A/B: -10 us per step).
 int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, int K, int64_t N, float *C,
               const float *bias, int accum, hipStream_t st, int act = 0) {
     if (M <= 0 || N <= 0) return LRS_OK;
     if (M > 256 || lda < K || lda % 16) return LRS_E_UNSUPPORTED;
     const int Kp32 = (int)round_up(lda, 32), ldsrow = pw_ldsrow(Kp32);
-    // four row blocks (M > 192): 80-pixel workgroups (k_pw<4, 5>), whose grid fits one round of
-    // the 2-per-CU slots that kernel's registers allow where 64-pixel ones need 1.2 rounds
-    const bool wide = (M + 63) / 64 == 4 && pw_wide();
-    const int npx = wide ? 80 : 64;
-    const int lds = 3 * npx * ldsrow;
     static bool attr_set = false;
-    if (!attr_set) {   // up to K = 256: 3 x 64 (80) x 528 B
-        const int mx = 3 * 64 * pw_ldsrow(256);
-        hipError_t e = hipFuncSetAttribute((const void *)k_pw<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void *)k_pw<4>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void *)k_pw<4, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, 3 * 80 * pw_ldsrow(256));
-        if (e != hipSuccess) return (int)e;
+    if (!attr_set) {   // up to K = 256: 3 x 80 x 528 B
+        const int mx = 3 * 80 * pw_ldsrow(256);
+        for (const PwKernel &k : kPwKernels) {
+            const hipError_t e = hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            if (e != hipSuccess) return (int)e;
+        }
         attr_set = true;
     }
     if (Kp32 > 256 || (int64_t)K * N * 4 >= kOob || 3 * pstride * 2 >= kOob) return LRS_E_UNSUPPORTED;
     static const int dbg = getenv("LRS_PW_DBG") ? atoi(getenv("LRS_PW_DBG")) : 0;
     const PwArgs a{A, pstride, lda, B, K, N, C, bias, M, Kp32, ldsrow, accum, dbg, act};
-    const dim3 grid((unsigned)((N + npx - 1) / npx));
-    switch ((M + 63) / 64) {
-    case 1: hipLaunchKernelGGL(k_pw<1>, grid, dim3(256), lds, st, a); break;
-    case 2: hipLaunchKernelGGL(k_pw<2>, grid, dim3(256), lds, st, a); break;
-    case 3: hipLaunchKernelGGL(k_pw<3>, grid, dim3(256), lds, st, a); break;
-    default:
-        if (wide) hipLaunchKernelGGL((k_pw<4, 5>), grid, dim3(256), lds, st, a);
-        else hipLaunchKernelGGL(k_pw<4>, grid, dim3(256), lds, st, a);
-        break;
+    const int mt = (M + 63) / 64;
+    const PwKernel *best = nullptr;
+    int64_t best_cost = 0;
+    for (const PwKernel &k : kPwKernels) {
+        if (k.mt != mt || !pw_nb_allowed(k.nb)) continue;
+        const int lds = 3 * 16 * k.nb * ldsrow;
+        const int per_cu = std::min(k.wg_per_cu, (160 * 1024) / lds);
+        const int64_t wgs = (N + 16 * k.nb - 1) / (16 * k.nb);
+        const int64_t rounds = (wgs + 256 * per_cu - 1) / (256 * per_cu);
+        const int64_t cost = rounds * k.nb;
+        if (!best || cost < best_cost || (cost == best_cost && k.nb > best->nb)) {
+            best = &k;
+            best_cost = cost;
+        }
     }
+    if (!best) return LRS_E_UNSUPPORTED;
+    const int npx = 16 * best->nb;
+    hipLaunchKernelGGL(best->fn, dim3((unsigned)((N + npx - 1) / npx)), dim3(256), 3 * npx * ldsrow, st, a);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
