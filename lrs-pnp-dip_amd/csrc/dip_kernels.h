@@ -1233,7 +1233,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd_r(BnBwdArgs a) {
 // Gram on the smaller side (m = min(rows, cols) <= 128) in fp64, exact products.
 // ------------------------------------------------------------------------------------------
 constexpr int kSnMaxDim = 128;
-constexpr int kSnSplit = 16;  // inner-dimension split of the Gram (partials reduced by k_sn_gram_reduce)
+constexpr int kSnSplit = 16;  // inner-dimension split of the Gram (partials reduced by k_sn_gram_reduce; 32: slower)
 constexpr int kSnPairs = 36;  // upper 16 x 16 tile pairs of a 128 x 128 Gram
 // Gram workspace per conv (doubles): the reduced symmetric Gram [128][128], then the split
 // partials [kSnSplit][kSnPairs][16 * 16]
@@ -1279,8 +1279,9 @@ __device__ __forceinline__ void sn_gram_body(const SnConv &cv, float (*Ws)[36], 
     sn_d4 acc[9];
 #pragma unroll
     for (int u = 0; u < 9; ++u) acc[u] = sn_d4{0.0, 0.0, 0.0, 0.0};
-    for (int k0 = kb; k0 < ke; k0 += 32) {
-        float v[16];
+    // the next chunk's global loads are issued before this chunk's MFMAs
+    float v[16];
+    auto load = [&](int k0) {
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             const int e = t + 256 * u;
@@ -1288,6 +1289,9 @@ __device__ __forceinline__ void sn_gram_body(const SnConv &cv, float (*Ws)[36], 
             const int k = k0 + kk;
             v[u] = (r < m && k < ke) ? (rowside ? cv.W[(int64_t)r * cv.cols + k] : cv.W[(int64_t)k * cv.cols + r]) : 0.f;
         }
+    };
+    if (kb < ke) load(kb);
+    for (int k0 = kb; k0 < ke; k0 += 32) {
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
@@ -1296,6 +1300,7 @@ __device__ __forceinline__ void sn_gram_body(const SnConv &cv, float (*Ws)[36], 
             Ws[r][kk] = v[u];
         }
         __syncthreads();
+        if (k0 + 32 < ke) load(k0 + 32);
 #pragma unroll
         for (int kq = 0; kq < 32; kq += 4) {
             double f[8];
