@@ -202,6 +202,8 @@ def cpu_baseline_pnp(Y, M, D, bb, nit, budget_s):
     t_admm = cpu_admm(Y, M, bb)
     t_iter = t_sc + t_svt + t_admm
     return {"value": 1.0 / t_iter, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+            # the GPU path computes alpha once per observation pattern, outside the timed steps
+            "value_alpha_hoisted": 1.0 / (t_iter - t_alpha),
             "sample": f"{done} of {nb} blocks (alpha+ISTA, Nit={nit}) extrapolated x{nb / done:.1f} "
                       f"({t_sc:.1f}s, of which per-block alpha {t_alpha:.1f}s), + full SVT ({t_svt:.2f}s) + "
                       f"full ADMM update ({t_admm:.3f}s); est. {t_iter:.1f}s per outer iteration"}
@@ -231,8 +233,11 @@ def cpu_baseline_dip(solver, Y, M, D, bb, nit, dip_steps, budget_s):
     t_admm = cpu_admm(Y, M, bb)
     t_iter = t_sc + per_step * dip_steps + t_admm
     return {"value": 1.0 / t_iter, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+            # the GPU path computes alpha once per observation pattern, outside the timed steps
+            "value_alpha_hoisted": 1.0 / (t_iter - t_alpha),
             "sample": f"sparse coding: {done} of {nb} blocks (alpha+ISTA, Nit={nit}, oracle C) extrapolated "
-                      f"x{nb / done:.1f} = {t_sc:.1f}s; DIP: {steps} training steps of the torch-CPU restatement "
+                      f"x{nb / done:.1f} = {t_sc:.1f}s (of which per-block alpha {t_alpha:.1f}s, as the reference "
+                      f"computes it inside ista; value_alpha_hoisted leaves it out); DIP: {steps} training steps of the torch-CPU restatement "
                       f"(oracle/dip_ref.py: conv/BN/LeakyReLU, full-SVD sigma_max per conv, Adam) at "
                       f"{per_step:.2f}s/step x {dip_steps} = {per_step * dip_steps:.1f}s; full ADMM update "
                       f"{t_admm:.3f}s; est. {t_iter:.1f}s per outer iteration"}
