@@ -65,7 +65,7 @@ static int g_dip_gemm_precision = LRS_DIP_SPLIT_BF16;
 // then split K until ~512 workgroups (2 per CU), keeping >= 128 of K per split and <= 64 splits.
 // (Measured with the f32 kernels: 128-tiles with deeper split-K on the small-N weight-gradient
 // GEMMs, or a 1024-WG target, are slower at both the 36x36 and the 196x196 sizes.)
-Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision, bool force_big = false) {
+Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision, bool force_big = false, int target = 512) {
     const int64_t t128 = (int64_t)((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
     // long-K GEMMs (the weight gradients, K = pixels) take 128-tiles with deep split-K on the
     // split-bf16 path when that still gives >= 256 workgroups (measured 25-30 % faster at 196^2 and
@@ -77,7 +77,7 @@ Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision, bo
     const int64_t tiles = big ? t128 : (int64_t)((M + kBM64 - 1) / kBM64) * ((N + kBN64 - 1) / kBN64);
     int S = 1;
     if (tiles < 256) {
-        S = (int)((512 + tiles - 1) / tiles);   // ~2 workgroups per CU (256 and 1024 measured slower)
+        S = (int)((target + tiles - 1) / tiles);   // ~2 workgroups per CU (256 and 1024 measured slower)
         const int smax = deep ? K / 512 : (K + 127) / 128;
         if (S > smax) S = smax;
         if (S > (deep ? 256 : 64)) S = deep ? 256 : 64;
@@ -319,11 +319,21 @@ inline int64_t wprep_elems(const ConvGeom &g, int Cout) {
 
 // Implicit-GEMM conv product on the split-bf16 kernel, with the same split-K / reduce tail as
 // gemm().
+// split-K workgroup target of a forward conv whose partials a fused BN kernel finishes: fewer
+// splits than the GEMMs' 512 (the BN kernel, one workgroup per channel, re-reads every partial):
+// 196^2 step 1.336 -> 1.312 ms at 384 (A/B on one box: 256 1.317, 320 1.313).  The workspace is
+// sized for 512, so a larger LRS_DIP_FWD_SPLIT_WG (tuning only) fails with LRS_E_WORKSPACE.
+inline int fwd_split_target() {
+    static const int v = getenv("LRS_DIP_FWD_SPLIT_WG") ? std::max(1, atoi(getenv("LRS_DIP_FWD_SPLIT_WG"))) : 384;
+    return v;
+}
+
 template <class LA, class LB>
 int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const float *div, int M, int N, int K,
-                 float *part, int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr, int accum = 0) {
+                 float *part, int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr, int accum = 0,
+                 int target = 512) {
     if (M <= 0 || N <= 0) return LRS_OK;
-    const Split s = choose_split(M, N, K, LRS_DIP_SPLIT_BF16, true);
+    const Split s = choose_split(M, N, K, LRS_DIP_SPLIT_BF16, true, target);
     if (nsplit_out) *nsplit_out = s.S;
     GemmArgs g{nullptr, nullptr, C, bias, div, M, N, K, s.kchunk, accum};
     if (s.S > 1) {
@@ -347,7 +357,7 @@ int upc_fwd(const ConvGeom &g, const float *x, const __bf16 *wpre, const float *
             int64_t part_cap, hipStream_t st, int *nsplit_out) {
     const int Cp = r16(g.Cin), Q = g.Hs * g.Ws, K = 4 * Cp;
     const int64_t P = (int64_t)g.Ho * g.Wo;
-    const Split s = choose_split(Cout, 4 * Q, K, LRS_DIP_SPLIT_BF16, true);
+    const Split s = choose_split(Cout, 4 * Q, K, LRS_DIP_SPLIT_BF16, true, nsplit_out ? fwd_split_target() : 512);
     if (nsplit_out) *nsplit_out = s.S;
     GemmArgs a{nullptr, nullptr, y, bias, nullptr, Cout, Q, K, s.kchunk, 0, 4, g.Ws, g.Wo, P};
     if (s.S > 1) {
@@ -510,7 +520,7 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
         const int kk = g.k * g.k, Cp = r16(g.Cin);
         return gemm_s3_conv(LdPre{wpre, (int64_t)Cout * kk * Cp, kk * Cp, Cout},
                             LdFwdTM{x, g.Cin * g.Hs * g.Ws * 4, g, Cp, nullptr}, y, bias, nullptr, Cout, P, kk * Cp,
-                            part, part_cap, st, nsplit_out);
+                            part, part_cap, st, nsplit_out, 0, nsplit_out ? fwd_split_target() : 512);
     }
     if (!plain_unit(g)) {
         const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min(Kc, 65535));
