@@ -305,7 +305,8 @@ def main_dip(args, ctx):
         if per is not None:
             dip_ms = per[0][0]
             ista_ms = float(np.nanmean([v[1] for v in per[1:]]))
-    flops = dip_flops_per_step(s.dip.net) * args.dip_steps
+    # (task-parallel workers build no DIP engine; rank 0, which prints the line, always has one)
+    flops = dip_flops_per_step(s.dip.net) * args.dip_steps if s.dip is not None else float("nan")
     profiled = not (args.cube or args.bb or args.nit or args.K != 256 or args.dip_steps != 100)
     achieved = flops / (dip_ms * 1e-3) / 1e12
     n = bb * bb

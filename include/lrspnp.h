@@ -5,7 +5,8 @@
  * device pointer is caller-owned; the library never allocates (workspaces are sized by the
  * `*_workspace` queries and passed in).  Calls are stream-ordered and reentrant, never
  * synchronise the host, and return 0 (LRS_OK), a negative LRS_E_* code, or a positive
- * hipError_t.  Arrays are float32 row-major unless noted.
+ * hipError_t.  Arrays are float32 row-major unless noted.  Modes are per call (lrs_ista_opts,
+ * lrs_dip_opts) or per handle; no exported function changes process-wide state.
  *
  * Reference interfaces replaced (shuoli0708/LRS-PnP-DIP; file:line):
  *   lrs_nlm_col_f32       skimage.restoration.denoise_nl_means(g, h, fast_mode=True,
@@ -95,39 +96,43 @@ int lrs_ista_alpha_f32(const float *D, int64_t n, int64_t K, const uint8_t *obs_
  * (lrs_ista_workspace bytes; LRS_E_WORKSPACE when too small).
  * Replaces the per-block loop of main_LRS_PnP.py:270-303 / main_LRS_PnP_DIP_1-LiP.py:367-392
  * around ista() (main_LRS_PnP.py:131-149, …1-LiP.py:185-198) and delete_element (:201-204). */
+/* Per-call options (NULL = defaults).  precision: arithmetic of the two products of the resident
+ * (n_pad <= 64) kernel: LRS_ISTA_SPLIT_BF16 (default): bf16 matrix cores on operands split exactly
+ * into three bf16 terms (six partial products, fp32 accumulation: fp32-GEMM accuracy, not bitwise
+ * the f32 MFMA); LRS_ISTA_F32: v_mfma_f32_16x16x4_f32 (exact f32 products).  The NLM prox is
+ * identical.  The library keeps no process-wide mode. */
+#define LRS_ISTA_F32 0
+#define LRS_ISTA_SPLIT_BF16 1
+typedef struct {
+    int32_t precision;
+    int32_t reserved[7];
+} lrs_ista_opts;
 size_t lrs_ista_workspace(int64_t n, int64_t K, int prox);
 int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,
                  int64_t K, int64_t nb, const float *alpha, const double *thr, int Nit, int prox,
-                 float *coefs, float *phi, void *ws, size_t ws_bytes, void *stream);
-/* Column tiles (16 blocks each) per wave of the row-split kernel at 129 <= K <= 256: 1 (default,
- * more waves) or 2 (each dictionary fragment serves 32 blocks).  Process-wide. */
-int lrs_ista_set_rs_cols(int cols);
+                 float *coefs, float *phi, const lrs_ista_opts *opts, void *ws, size_t ws_bytes,
+                 void *stream);
 /* NLmeansfilter(g, 3, 3, h) (LRS-PnP(Matlab Code)/NLmeansfilter.m:18-78, the prox of
  * pnp_ista.m:30) of nvec columns of length K, fp64, 'symmetric' padding. */
 int lrs_nlm_matlab_col_f32(const float *g, int64_t ldg, float *out, int64_t ldo, int64_t K,
                            int64_t nvec, double h, const double *h_per_vec, void *stream);
-/* Arithmetic of the two products of the resident (n_pad <= 64) kernel, process-wide:
- * LRS_ISTA_SPLIT_BF16 (default): bf16 matrix cores on operands split exactly into three bf16
- * terms (six partial products, fp32 accumulation: fp32-GEMM accuracy, not bitwise the f32 MFMA);
- * LRS_ISTA_F32: v_mfma_f32_16x16x4_f32 (exact f32 products).  The NLM prox is identical. */
-#define LRS_ISTA_F32 0
-#define LRS_ISTA_SPLIT_BF16 1
-int lrs_ista_set_precision(int precision);
-int lrs_ista_get_precision(void);
-
-/* Arithmetic of the DIP engine's large conv GEMMs (128x128 tiles), process-wide:
- * LRS_DIP_SPLIT_BF16 (default): bf16 matrix cores on operands split into three bf16 terms, six
- * partial products, fp32 accumulation (fp32-GEMM accuracy); LRS_DIP_F32: v_mfma_f32_16x16x4_f32. */
+/* Options of the DIP engine and the conv primitives (NULL = defaults), fixed per call or, for a
+ * lrs_dipnet, at creation -- the library keeps no process-wide mode:
+ *   precision: arithmetic of the conv GEMMs.  LRS_DIP_SPLIT_BF16 (default): bf16 matrix cores on
+ *     operands split into three bf16 terms, six partial products, fp32 accumulation (fp32-GEMM
+ *     accuracy); LRS_DIP_F32: v_mfma_f32_16x16x4_f32 (the explicit-im2col kernels; a lrs_dipnet
+ *     created with it runs every conv on them).
+ *   upsample_dgrad: data gradient of an upsampled stride-1 conv (nearest x2, then 2x2 unpadded or
+ *     3x3 pad 1): 0 (default) = correlation over the padded upsampled domain + fold; 1 = a stride-2
+ *     conv with the (k+1)x(k+1) effective kernel on the source grid (2.25x fewer products) +
+ *     reflection border terms.  lrs_conv2d_workspace must be queried with the same options. */
 #define LRS_DIP_F32 0
 #define LRS_DIP_SPLIT_BF16 1
-int lrs_dip_set_precision(int precision);
-int lrs_dip_get_precision(void);
-/* Data gradient of an upsampled stride-1 conv (nearest x2, then 2x2 unpadded or 3x3 pad 1):
- * 0 (default) = correlation over the padded upsampled domain + fold; 1 = a stride-2 conv with the
- * (k+1)x(k+1) effective kernel on the source grid (2.25x fewer products) + reflection border
- * terms.  Process-wide; a lrs_dipnet fixes its layout at creation, the lrs_conv2d_* workspace
- * sizes follow the current mode. */
-int lrs_dip_set_upsample_dgrad(int mode);
+typedef struct {
+    int32_t precision;
+    int32_t upsample_dgrad;
+    int32_t reserved[6];
+} lrs_dip_opts;
 
 /* ---- SVT low-rank prox ---------------------------------------------------------------------
  * U = SVT(Z, tau) with Z = X + c2 * L2 (c2 = float(1/mu_2); L2 may be NULL), via an fp64 Gram
@@ -201,20 +206,23 @@ int64_t lrs_conv2d_col_size(int Cin, int H, int W, int k, int stride, int pad, i
  * the backward); col == NULL (k <= 3): implicit GEMM, the im2col is gathered inside the
  * split-bf16 kernel and never stored (backward: lrs_conv2d_bwd_x_f32).
  * ws/ws_bytes: split-K partials (lrs_conv2d_workspace). */
-size_t lrs_conv2d_workspace(int Cin, int H, int W, int Cout, int k, int stride, int pad, int upsample);
+size_t lrs_conv2d_workspace(int Cin, int H, int W, int Cout, int k, int stride, int pad, int upsample,
+                            const lrs_dip_opts *opts);
 int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const float *w, const float *bias,
                        int Cout, int k, int stride, int pad, int pad_mode, int upsample, float *col,
-                       float *y, void *ws, size_t ws_bytes, void *stream);
+                       float *y, const lrs_dip_opts *opts, void *ws, size_t ws_bytes, void *stream);
 /* gw = (gy col^T) / *w_div (w_div nullable, device scalar: the spectral-norm scale);
  * gx (nullable) = adjoint of the im2col of gy through w.  gbias is produced by lrs_bn_act_bwd.
  * col = the forward's col (or x itself for a plain 1x1 unit). */
 int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float *w, const float *w_div, int Cin,
                        int H, int W, int Cout, int k, int stride, int pad, int pad_mode, int upsample,
-                       float *gx, float *gw, void *ws, size_t ws_bytes, void *stream);
+                       float *gx, float *gw, const lrs_dip_opts *opts, void *ws, size_t ws_bytes,
+                       void *stream);
 /* The same from the conv input x (k <= 3): gw's col^T is gathered inside the GEMM. */
 int lrs_conv2d_bwd_x_f32(const float *gy, const float *x, const float *w, const float *w_div, int Cin,
                          int H, int W, int Cout, int k, int stride, int pad, int pad_mode, int upsample,
-                         float *gx, float *gw, void *ws, size_t ws_bytes, void *stream);
+                         float *gx, float *gw, const lrs_dip_opts *opts, void *ws, size_t ws_bytes,
+                         void *stream);
 
 /* y = act(BN_lip(z)) with batch statistics (gamma == NULL: y = act(z)).  Saves mean / invstd
  * [C]; running stats (nullable) get the momentum update.  ws: lrs_bn_act_workspace bytes,
@@ -277,7 +285,10 @@ typedef struct {
     int32_t kind, in0, in1, cout, k, stride, pad, pad_mode, upsample, bn, act, sn, winit;
 } lrs_dip_node;
 typedef struct lrs_dipnet lrs_dipnet;
-int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, int H, int W, lrs_dipnet **out);
+int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, int H, int W, const lrs_dip_opts *opts,
+                      lrs_dipnet **out);
+/* the options the net was created with */
+int lrs_dipnet_get_opts(const lrs_dipnet *net, lrs_dip_opts *opts);
 void lrs_dipnet_destroy(lrs_dipnet *net);
 int64_t lrs_dipnet_num_params(const lrs_dipnet *net);
 int64_t lrs_dipnet_num_bnstats(const lrs_dipnet *net);

@@ -23,6 +23,27 @@ namespace {
 
 constexpr int kEw = 256;   // elementwise block size
 
+// A/B tuning knobs.  The environment is read only by the tuning build (make TUNING=1 ->
+// liblrspnp_hip_tune.so, -DLRS_TUNING); the product library always takes the default, so a
+// variable left set on a production box cannot change its arithmetic path.
+inline int64_t tune_knob(const char *name, int64_t dflt) {
+#ifdef LRS_TUNING
+    const char *e = getenv(name);
+    return e ? atoll(e) : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
+}
+inline const char *tune_str(const char *name) {
+#ifdef LRS_TUNING
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 inline unsigned ew_blocks(int64_t n, int64_t cap = 4096) {
     int64_t b = (n + kEw - 1) / kEw;
     if (b < 1) b = 1;
@@ -30,7 +51,19 @@ inline unsigned ew_blocks(int64_t n, int64_t cap = 4096) {
     return (unsigned)b;
 }
 
-int make_geom(int Cin, int H, int W, int k, int stride, int pad, int pad_mode, int up, ConvGeom &g) {
+// the defaults of a NULL lrs_dip_opts
+inline lrs_dip_opts dip_opts(const lrs_dip_opts *o) {
+    lrs_dip_opts d{};
+    d.precision = LRS_DIP_SPLIT_BF16;
+    d.upsample_dgrad = 0;
+    return o ? *o : d;
+}
+
+int make_geom(int Cin, int H, int W, int k, int stride, int pad, int pad_mode, int up, ConvGeom &g,
+              const lrs_dip_opts *opts = nullptr) {
+    const lrs_dip_opts o = dip_opts(opts);
+    if (o.precision != LRS_DIP_F32 && o.precision != LRS_DIP_SPLIT_BF16) return LRS_E_INVALID;
+    if (o.upsample_dgrad != 0 && o.upsample_dgrad != 1) return LRS_E_INVALID;
     if (Cin <= 0 || H <= 0 || W <= 0 || k <= 0 || stride <= 0 || pad < 0) return LRS_E_INVALID;
     if (pad_mode != LRS_PAD_ZERO && pad_mode != LRS_PAD_REFLECT) return LRS_E_INVALID;
     g.Cin = Cin;
@@ -48,6 +81,13 @@ int make_geom(int Cin, int H, int W, int k, int stride, int pad, int pad_mode, i
     if (hp < k || wp < k) return LRS_E_INVALID;
     g.Ho = (hp - k) / stride + 1;
     g.Wo = (wp - k) / stride + 1;
+    g.prec = o.precision;
+    // effective kernel of the upsampled data gradient as a stride-2 conv on the source grid
+    g.ke = 0;
+    if (o.upsample_dgrad && g.up && g.stride == 1 && g.Hs >= 2 && g.Ws >= 2) {
+        if (g.k == 3 && g.pad == 1) g.ke = 4;
+        if (g.k == 2 && g.pad == 0) g.ke = 3;
+    }
     return LRS_OK;
 }
 
@@ -58,14 +98,11 @@ struct Split {
     bool big;   // 128x128 tiles (k_gemm) or 64x64 (k_gemm64)
 };
 
-// product arithmetic of the 128x128 conv GEMMs: LRS_DIP_SPLIT_BF16 (default) or LRS_DIP_F32
-static int g_dip_gemm_precision = LRS_DIP_SPLIT_BF16;
-
 // Tile choice and split-K: 128x128 tiles when they alone give >= 64 workgroups, else 64x64;
 // then split K until ~512 workgroups (2 per CU), keeping >= 128 of K per split and <= 64 splits.
 // (Measured with the f32 kernels: 128-tiles with deeper split-K on the small-N weight-gradient
 // GEMMs, or a 1024-WG target, are slower at both the 36x36 and the 196x196 sizes.)
-Split choose_split(int M, int N, int K, int precision = g_dip_gemm_precision, bool force_big = false, int target = 512) {
+Split choose_split(int M, int N, int K, int precision = LRS_DIP_SPLIT_BF16, bool force_big = false, int target = 512) {
     const int64_t t128 = (int64_t)((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
     // long-K GEMMs (the weight gradients, K = pixels) take 128-tiles with deep split-K on the
     // split-bf16 path when that still gives >= 256 workgroups (measured 25-30 % faster at 196^2 and
@@ -104,19 +141,20 @@ int64_t gemm_part_floats(int M, int N, int K) {
     return S > 1 ? (int64_t)S * M * N : 0;
 }
 
-// C = op(A) op(B) (+ bias) (/ *div); part: split-K scratch (>= gemm_part_floats)
-int gemm(int TA, int TB, const float *A, const float *B, float *C, const float *bias, const float *div, int M,
+// C = op(A) op(B) (+ bias) (/ *div); part: split-K scratch (>= gemm_part_floats); prec: the
+// conv's ConvGeom::prec
+int gemm(int prec, int TA, int TB, const float *A, const float *B, float *C, const float *bias, const float *div, int M,
          int N, int K, float *part, int64_t part_cap, hipStream_t st, int accum = 0, int *nsplit_out = nullptr,
          bool force_big = false) {
     if (M <= 0 || N <= 0) return LRS_OK;
-    const Split s = choose_split(M, N, K, g_dip_gemm_precision, force_big);
+    const Split s = choose_split(M, N, K, prec, force_big);
     if (nsplit_out) *nsplit_out = s.S;   // > 1: the caller finishes the split-K sum (no reduce here)
     GemmArgs g{A, B, C, bias, div, M, N, K, s.kchunk, accum};
     if (s.S > 1) {
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
         g.C = part;
     }
-    if (s.big && g_dip_gemm_precision == LRS_DIP_SPLIT_BF16) {
+    if (s.big && prec == LRS_DIP_SPLIT_BF16) {
         dim3 grid((N + kBN - 1) / kBN, (M + kBM - 1) / kBM, s.S);
         const int lda = TA ? M : K, ldb = TB ? K : N;
         if (!TA && !TB)
@@ -162,35 +200,31 @@ inline int r16(int x) { return (x + 15) & ~15; }
 // Off by default: measured in the whole 196^2 training step (bench configs[2], 2 x 2 A/B runs) it is
 // ~1 % slower than the padded-domain correlation + fold -- the up_4 data-gradient work it saves ran
 // beside that layer's weight gradient anyway, and it adds a split-K reduce and the border launches
-// to the critical chain.  lrs_dip_set_upsample_dgrad(1) selects it (tests cover both).
+// to the critical chain.  lrs_dip_opts::upsample_dgrad = 1 selects it (tests cover both).
 // An upsampled, reflection-padded 3 x 3 stride-1 conv runs by output parity class in the network
 // engine (dip_gemm.h LdUpFwdTM / LdUpDgradTM, 4/9 of the direct products).  LRS_DIP_UPC=0 keeps the
 // direct implicit GEMM over the upsampled grid (A/B only).
 inline bool upc_conv(const ConvGeom &g) {
-    static const bool on = !getenv("LRS_DIP_UPC") || atoi(getenv("LRS_DIP_UPC")) != 0;
+    static const bool on = tune_knob("LRS_DIP_UPC", 1) != 0;
     return on && g.up && g.k == 3 && g.pad == 1 && g.pad_mode == LRS_PAD_REFLECT && g.stride == 1 && g.Hs >= 2 &&
            g.Ws >= 2;
 }
 
-static int g_dip_upeff = 0;
-inline int up_eff_k(const ConvGeom &g) {
-    if (!g_dip_upeff || !g.up || g.stride != 1 || g.Hs < 2 || g.Ws < 2) return 0;
-    if (g.k == 3 && g.pad == 1) return 4;
-    if (g.k == 2 && g.pad == 0) return 3;
-    return 0;
-}
+// fixed with the geometry (make_geom, lrs_dip_opts::upsample_dgrad): the workspace size, the
+// weight-preparation table and the backward all read this one value
+inline int up_eff_k(const ConvGeom &g) { return g.ke; }
 // ---- small-map convs on k_conv_sm (dip_sm.h) ------------------------------------------------
 // A conv runs there when it is not 1x1, k <= 3 and its output map is below implicit_min_pixels()
 // (the maps that had the explicit im2col path).  LRS_DIP_SM=0 keeps the explicit path (A/B only).
 inline bool sm_enabled() {
-    static const bool v = !getenv("LRS_DIP_SM") || atoi(getenv("LRS_DIP_SM")) != 0;
+    static const bool v = tune_knob("LRS_DIP_SM", 1) != 0;
     return v;
 }
 
 // 64 x 64 tiles; split K so that the grid has ~sm_target() workgroups (k per split a multiple of
 // 64).  LRS_DIP_SM_WG overrides the target (tuning only).
 inline int64_t sm_target() {
-    static const int64_t v = getenv("LRS_DIP_SM_WG") ? std::max(1LL, atoll(getenv("LRS_DIP_SM_WG"))) : 640;
+    static const int64_t v = std::max<int64_t>(1, tune_knob("LRS_DIP_SM_WG", 640));
     return v;
 }
 Split sm_split(int M, int N, int K) {
@@ -324,7 +358,7 @@ inline int64_t wprep_elems(const ConvGeom &g, int Cout) {
 // 196^2 step 1.336 -> 1.312 ms at 384 (A/B on one box: 256 1.317, 320 1.313).  The workspace is
 // sized for 512, so a larger LRS_DIP_FWD_SPLIT_WG (tuning only) fails with LRS_E_WORKSPACE.
 inline int fwd_split_target() {
-    static const int v = getenv("LRS_DIP_FWD_SPLIT_WG") ? std::max(1, atoi(getenv("LRS_DIP_FWD_SPLIT_WG"))) : 384;
+    static const int v = (int)std::max<int64_t>(1, tune_knob("LRS_DIP_FWD_SPLIT_WG", 384));
     return v;
 }
 
@@ -427,7 +461,7 @@ inline bool conv_implicit_ok(const ConvGeom &g, int Cout) {
 // faster (measured at 36x36: 1.23 vs 1.41 ms per U-Net step).  LRS_DIP_IMPLICIT_MIN_P overrides
 // (tuning only).
 inline int64_t implicit_min_pixels() {
-    static const int64_t v = getenv("LRS_DIP_IMPLICIT_MIN_P") ? atoll(getenv("LRS_DIP_IMPLICIT_MIN_P")) : 2048;
+    static const int64_t v = tune_knob("LRS_DIP_IMPLICIT_MIN_P", 2048);
     return v;
 }
 
@@ -441,7 +475,7 @@ void wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, 
 
 // LRS_DIP_PW_NB = the allowed NB digits, e.g. "4" keeps 64-pixel workgroups everywhere (A/B only)
 inline bool pw_nb_allowed(int nb) {
-    static const char *v = getenv("LRS_DIP_PW_NB");
+    static const char *v = tune_str("LRS_DIP_PW_NB");
     return !v || strchr(v, '0' + nb) != nullptr;
 }
 
@@ -478,7 +512,7 @@ int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, 
         attr_set = true;
     }
     if (Kp32 > 256 || (int64_t)K * N * 4 >= kOob || 3 * pstride * 2 >= kOob) return LRS_E_UNSUPPORTED;
-    static const int dbg = getenv("LRS_PW_DBG") ? atoi(getenv("LRS_PW_DBG")) : 0;
+    static const int dbg = (int)tune_knob("LRS_PW_DBG", 0);
     const PwArgs a{A, pstride, lda, B, K, N, C, bias, M, Kp32, ldsrow, accum, dbg, act};
     const int mt = (M + 63) / 64;
     const PwKernel *best = nullptr;
@@ -527,7 +561,7 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
         hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, st, x, g, col);
         B = col;
     }
-    return gemm(0, 0, w, B, y, bias, nullptr, Cout, P, Kc, part, part_cap, st, 0, nsplit_out);
+    return gemm(g.prec, 0, 0, w, B, y, bias, nullptr, Cout, P, Kc, part, part_cap, st, 0, nsplit_out);
 }
 
 // gw = gz col^T / div ; gx = col2im(w^T gz) (gw, gx nullable).  dcol: Kc*P floats when !plain.
@@ -551,13 +585,13 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         // kernel (A/B in the 196^2 training step, configs[2]: 5.50 -> 5.65 outer it/s against the f32
         // 64-tile kernel; alone the two are within 12 %, but the f32 kernel's 512 workgroups hold the
         // CUs the concurrent data-gradient chain needs for longer)
-        rc = gemm(0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st, 0, nullptr, plain_unit(g));
+        rc = gemm(g.prec, 0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st, 0, nullptr, plain_unit(g));
     }
     if (rc || !gx) return rc;
     if (plain_unit(g) && wpre)      // 1x1 data gradient: W^T planes (wprep's WD)
         return pw_launch(wpre + wprep_fwd_elems(g, Cout), (int64_t)g.Cin * r16(Cout), r16(Cout), g.Cin, gz, Cout, P,
                          gx, nullptr, accum_gx, st);
-    if (plain_unit(g)) return gemm(1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st, accum_gx);
+    if (plain_unit(g)) return gemm(g.prec, 1, 0, w, gz, gx, nullptr, nullptr, Kc, P, Cout, part, part_cap, st, accum_gx);
     const int ke = up_eff_k(g);
     const bool refl_border = g.pad_mode == LRS_PAD_REFLECT && g.k == 3;
     const int Lmax = std::max(g.Ws, g.Hs);
@@ -606,7 +640,7 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         LRS_CHECK_LAUNCH();
         return LRS_OK;
     }
-    rc = gemm(1, 0, w, gz, dcol, nullptr, nullptr, Kc, P, Cout, part, part_cap, st);
+    rc = gemm(g.prec, 1, 0, w, gz, dcol, nullptr, nullptr, Kc, P, Cout, part, part_cap, st);
     if (rc) return rc;
     const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
     if (g.stride == 1) hipLaunchKernelGGL(k_col2im<1>, grid, dim3(256), 0, st, dcol, g, gx, accum_gx);
@@ -632,8 +666,7 @@ inline bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 // thread for a channel of P pixels, or 0 where the S-way split / the P <= 4096 kernels are used.
 // LRS_DIP_BNREG_MAX_P overrides the upper limit (tuning only; 0 disables).
 inline int bn_reg_q(int64_t P, bool vec) {
-    static const int64_t maxp = getenv("LRS_DIP_BNREG_MAX_P") ? atoll(getenv("LRS_DIP_BNREG_MAX_P"))
-                                                              : (int64_t)4 * kBn1Threads * kBnRegMaxQ;
+    static const int64_t maxp = tune_knob("LRS_DIP_BNREG_MAX_P", (int64_t)4 * kBn1Threads * kBnRegMaxQ);
     if (!vec || P <= 4 * kBn1Threads || P > maxp || P > (int64_t)4 * kBn1Threads * kBnRegMaxQ) return 0;
     const int q = (int)((P + 4 * kBn1Threads - 1) / (4 * kBn1Threads));
     static const int qs[] = {2, 3, 4, 6, 8, 10};
@@ -804,18 +837,19 @@ inline ConvWs conv_ws(const ConvGeom &g, int Cout) {
     return w;
 }
 
-extern "C" size_t lrs_conv2d_workspace(int Cin, int H, int W, int Cout, int k, int stride, int pad, int upsample) {
+extern "C" size_t lrs_conv2d_workspace(int Cin, int H, int W, int Cout, int k, int stride, int pad, int upsample,
+                                       const lrs_dip_opts *opts) {
     ConvGeom g;
-    if (make_geom(Cin, H, W, k, stride, pad, LRS_PAD_ZERO, upsample, g) || Cout <= 0) return 0;
+    if (make_geom(Cin, H, W, k, stride, pad, LRS_PAD_ZERO, upsample, g, opts) || Cout <= 0) return 0;
     const ConvWs w = conv_ws(g, Cout);
     return (size_t)(w.dcol + w.part + w.wpre_floats) * sizeof(float) + 256;
 }
 
 extern "C" int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const float *w, const float *bias, int Cout,
                                   int k, int stride, int pad, int pad_mode, int upsample, float *col, float *y,
-                                  void *ws, size_t ws_bytes, void *stream) {
+                                  const lrs_dip_opts *opts, void *ws, size_t ws_bytes, void *stream) {
     ConvGeom g;
-    int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
+    int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g, opts);
     if (rc) return rc;
     if (!x || !w || !y || Cout <= 0) return LRS_E_INVALID;
     // col == NULL: implicit GEMM, or for a 1x1 conv the pointwise kernel on pre-split weights
@@ -832,9 +866,10 @@ extern "C" int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const f
 
 extern "C" int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float *w, const float *w_div, int Cin,
                                   int H, int W, int Cout, int k, int stride, int pad, int pad_mode, int upsample,
-                                  float *gx, float *gw, void *ws, size_t ws_bytes, void *stream) {
+                                  float *gx, float *gw, const lrs_dip_opts *opts, void *ws, size_t ws_bytes,
+                                  void *stream) {
     ConvGeom g;
-    int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
+    int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g, opts);
     if (rc) return rc;
     if (!gy || !col || !w || !gw || Cout <= 0) return LRS_E_INVALID;
     const ConvWs cw = conv_ws(g, Cout);
@@ -847,9 +882,10 @@ extern "C" int lrs_conv2d_bwd_f32(const float *gy, const float *col, const float
 
 extern "C" int lrs_conv2d_bwd_x_f32(const float *gy, const float *x, const float *w, const float *w_div, int Cin,
                                     int H, int W, int Cout, int k, int stride, int pad, int pad_mode, int upsample,
-                                    float *gx, float *gw, void *ws, size_t ws_bytes, void *stream) {
+                                    float *gx, float *gw, const lrs_dip_opts *opts, void *ws, size_t ws_bytes,
+                                    void *stream) {
     ConvGeom g;
-    int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
+    int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g, opts);
     if (rc) return rc;
     if (!gy || !x || !w || !gw || Cout <= 0) return LRS_E_INVALID;
     if (!conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
@@ -1051,6 +1087,7 @@ struct lrs_dipnet {
         float lr, b1, b2, eps;
     } key{};
     bool have_key = false;
+    lrs_dip_opts opts{};      // fixed at creation (precision, upsampled data-gradient form)
     float ln_lambda = 1.0f;   // W_used = W / max(1, sigma / ln_lambda)   (lipschitz_constraint_layer.py:42-44)
 
     float *f(int64_t off) const { return (float *)ws + off; }
@@ -1080,7 +1117,7 @@ bool bn_bwd_fusable(const lrs_dipnet *net, int j) {
 
 // workgroups per conv of the per-step weight preparation (LRS_DIP_PREP_WG overrides: tuning only)
 inline int prep_blocks() {
-    static const int v = getenv("LRS_DIP_PREP_WG") ? std::max(1, atoi(getenv("LRS_DIP_PREP_WG"))) : 512;
+    static const int v = (int)std::max<int64_t>(1, tune_knob("LRS_DIP_PREP_WG", 512));
     return v;
 }
 
@@ -1365,20 +1402,25 @@ void drop_graph(lrs_dipnet *net) {
 
 }  // namespace
 
-extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, int H, int W, lrs_dipnet **out) {
+extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, int H, int W,
+                                 const lrs_dip_opts *opts, lrs_dipnet **out) {
     if (!nodes || n_nodes <= 0 || C <= 0 || H <= 0 || W <= 0 || !out) return LRS_E_INVALID;
+    const lrs_dip_opts o = dip_opts(opts);
+    if (o.precision != LRS_DIP_F32 && o.precision != LRS_DIP_SPLIT_BF16) return LRS_E_INVALID;
+    if (o.upsample_dgrad != 0 && o.upsample_dgrad != 1) return LRS_E_INVALID;
     lrs_dipnet *net = new (std::nothrow) lrs_dipnet();
     if (!net) return LRS_E_INVALID;
     net->C0 = C;
     net->H = H;
     net->W = W;
     auto fail = [&](int rc) { delete net; return rc; };
-    net->implicit = g_dip_gemm_precision == LRS_DIP_SPLIT_BF16;
+    net->opts = o;
+    net->implicit = o.precision == LRS_DIP_SPLIT_BF16;
     // weight gradients on a side stream from 128^2 up: neutral alone at 196^2, but beside the
     // concurrent sparse-coding kernel the second stream keeps the DIP its share of the chip
     // (configs[2] 4.73 -> 5.19 outer it/s); slower at 36^2 (1.03 -> 1.19 ms per step)
     net->fork_w = (int64_t)H * W >= 16384;
-    if (const char *e = getenv("LRS_DIP_FORK")) net->fork_w = atoi(e) != 0;   // tuning / A/B only
+    net->fork_w = tune_knob("LRS_DIP_FORK", net->fork_w ? 1 : 0) != 0;   // tuning build only
     int64_t pofs = 0, rofs = 0, ofs = 0, max_dz = 0, max_dcol = 0, part = 0, max_bnpart = 0;
     int n_sn = 0;
     for (int i = 0; i < n_nodes; ++i) {
@@ -1391,7 +1433,7 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
         const int ci = net->tC(t0), hi = net->tH(t0), wi = net->tW(t0);
         if (N.d.kind == LRS_NODE_CONV) {
             if (N.d.cout <= 0) return fail(LRS_E_INVALID);
-            int rc = make_geom(ci, hi, wi, N.d.k, N.d.stride, N.d.pad, N.d.pad_mode, N.d.upsample, N.g);
+            int rc = make_geom(ci, hi, wi, N.d.k, N.d.stride, N.d.pad, N.d.pad_mode, N.d.upsample, N.g, &o);
             if (rc) return fail(rc);
             N.C = N.d.cout;
             N.H = N.g.Ho;
@@ -1730,16 +1772,8 @@ extern "C" int lrs_dipnet_last_loss(lrs_dipnet *net, double *loss, void *stream)
     return LRS_OK;
 }
 
-extern "C" int lrs_dip_set_precision(int precision) {
-    if (precision != LRS_DIP_F32 && precision != LRS_DIP_SPLIT_BF16) return LRS_E_INVALID;
-    g_dip_gemm_precision = precision;
-    return LRS_OK;
-}
-
-extern "C" int lrs_dip_get_precision(void) { return g_dip_gemm_precision; }
-
-extern "C" int lrs_dip_set_upsample_dgrad(int mode) {
-    if (mode != 0 && mode != 1) return LRS_E_INVALID;
-    g_dip_upeff = mode;
+extern "C" int lrs_dipnet_get_opts(const lrs_dipnet *net, lrs_dip_opts *opts) {
+    if (!net || !opts) return LRS_E_INVALID;
+    *opts = net->opts;
     return LRS_OK;
 }

@@ -1206,34 +1206,15 @@ __global__ __launch_bounds__(256) void k_nlm_col(const float *__restrict__ g, in
 
 using namespace lrs;
 
-// precision of the resident kernel's two products: LRS_ISTA_SPLIT_BF16 (default) or LRS_ISTA_F32
-static int g_ista_precision = LRS_ISTA_SPLIT_BF16;
-
-extern "C" int lrs_ista_set_precision(int precision) {
-    if (precision != LRS_ISTA_F32 && precision != LRS_ISTA_SPLIT_BF16) return LRS_E_INVALID;
-    g_ista_precision = precision;
-    return LRS_OK;
-}
-
-extern "C" int lrs_ista_get_precision(void) { return g_ista_precision; }
-
 // row-split kernel (csrc/ista_rs.hip): any n, K <= 512, every prox
 namespace lrs {
 size_t ista_rs_workspace(int64_t n, int64_t K);
 int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
                    const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi, void *ws,
-                   size_t ws_bytes, int cols_per_wave, hipStream_t st);
+                   size_t ws_bytes, hipStream_t st);
 int nlm_matlab_col_launch(const float *g, int64_t ldg, float *out, int64_t ldo, int64_t K, int64_t nvec, double h,
                           const double *h_per_vec, hipStream_t st);
 }  // namespace lrs
-
-static int g_ista_rs_cols = 1;   // column tiles (16 blocks) per wave of the row-split kernel
-
-extern "C" int lrs_ista_set_rs_cols(int cols) {
-    if (cols != 1 && cols != 2) return LRS_E_INVALID;
-    g_ista_rs_cols = cols;
-    return LRS_OK;
-}
 
 // The resident kernels (dictionary in LDS) serve n_pad <= 64 with K = 256 and the skimage / soft
 // prox; everything else runs the row-split kernel, which needs the fragment-ordered dictionary.
@@ -1249,8 +1230,11 @@ extern "C" size_t lrs_ista_workspace(int64_t n, int64_t K, int prox) {
 
 extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n,
                             int64_t n_pad, int64_t K, int64_t nb, const float *alpha, const double *thr,
-                            int Nit, int prox, float *coefs, float *phi, void *ws, size_t ws_bytes, void *stream) {
+                            int Nit, int prox, float *coefs, float *phi, const lrs_ista_opts *opts, void *ws,
+                            size_t ws_bytes, void *stream) {
     if (!Yb || !obs || !D || !alpha || !thr || !phi || n <= 0 || nb < 0 || Nit < 0 || K <= 0) return LRS_E_INVALID;
+    const int precision = opts ? opts->precision : LRS_ISTA_SPLIT_BF16;   // per call (no process state)
+    if (precision != LRS_ISTA_F32 && precision != LRS_ISTA_SPLIT_BF16) return LRS_E_INVALID;
     if (n_pad % 16 != 0 || n_pad < n) return LRS_E_INVALID;
     if (prox != LRS_PROX_NLM && prox != LRS_PROX_SOFT && prox != LRS_PROX_NLM_MATLAB) return LRS_E_INVALID;
     if (K > 512) return LRS_E_UNSUPPORTED;
@@ -1258,12 +1242,11 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     if (nb == 0) return LRS_OK;
     hipStream_t st = (hipStream_t)stream;
     if (!ista_resident(n_pad, K, prox))
-        return ista_rs_launch(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes,
-                              g_ista_rs_cols, st);
+        return ista_rs_launch(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, st);
     IstaParams p{Yb, obs, D, alpha, thr, coefs, phi, (int)n, (int)n_pad, Nit, prox, nb, 7.0};
     const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
     dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));
-    const bool split = g_ista_precision == LRS_ISTA_SPLIT_BF16;
+    const bool split = precision == LRS_ISTA_SPLIT_BF16;
     const dim3 grid_b3((unsigned)((nb + kB3Waves * 16 - 1) / (kB3Waves * 16)));
     if (split && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_b3<256, true>), grid_b3, dim3(kB3Threads), 0, st, p);

@@ -473,10 +473,12 @@ static int launch_rs(const IstaRsParams &p, int NT, hipStream_t st) {
 
 int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
                    const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi, void *ws,
-                   size_t ws_bytes, int cols_per_wave, hipStream_t st) {
+                   size_t ws_bytes, hipStream_t st) {
     if (K < 1 || K > 512) return LRS_E_UNSUPPORTED;
     const int NQ = rs_nq(K);
     const int NT = (int)(n_pad / 16);
+    // the dictionary images are addressed by 32-bit buffer offsets (t * NQ + k) * 1024
+    if ((int64_t)NT * NQ * 1024 >= ((int64_t)1 << 31)) return LRS_E_UNSUPPORTED;
     if (!ws || ws_bytes < ista_rs_workspace(n, K)) return LRS_E_WORKSPACE;
     float4 *DAf = reinterpret_cast<float4 *>(ws);
     float4 *DTf = DAf + (size_t)NT * NQ * 64;

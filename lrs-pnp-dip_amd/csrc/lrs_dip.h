@@ -8,6 +8,9 @@ namespace lrs {
 // -> pad (reflect / zero) -> k x k conv with stride -> [Cout][Ho][Wo].
 struct ConvGeom {
     int Cin, Hs, Ws, up, Hu, Wu, pad, pad_mode, k, stride, Ho, Wo;
+    // host-side mode, fixed when the geometry is made (lrs_dip_opts): the GEMM arithmetic of the
+    // explicit / 1x1 products, and the effective kernel size of the upsampled data gradient (0 = off)
+    int prec, ke;
 };
 
 struct SnConv {

@@ -24,6 +24,27 @@ class LrsError(RuntimeError):
     pass
 
 
+# per-call / per-handle options (include/lrspnp.h); the library keeps no process-wide mode
+ISTA_F32, ISTA_SPLIT_BF16 = 0, 1
+DIP_F32, DIP_SPLIT_BF16 = 0, 1
+
+
+class IstaOpts(ctypes.Structure):
+    _fields_ = [("precision", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+
+
+class DipOpts(ctypes.Structure):
+    _fields_ = [("precision", ctypes.c_int32), ("upsample_dgrad", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
+
+
+def ista_opts(precision: int = ISTA_SPLIT_BF16) -> IstaOpts:
+    return IstaOpts(precision=precision)
+
+
+def dip_opts(precision: int = DIP_SPLIT_BF16, upsample_dgrad: int = 0) -> DipOpts:
+    return DipOpts(precision=precision, upsample_dgrad=upsample_dgrad)
+
+
 _lib = None
 _device_checked = False
 
@@ -42,6 +63,7 @@ def _declare(L):
     c = ctypes
     vp, i64, i32, f32, f64, sz = c.c_void_p, c.c_int64, c.c_int, c.c_float, c.c_double, c.c_size_t
     i32p = c.POINTER(c.c_int32)
+    dop = c.POINTER(DipOpts)
     sig = {
         "lrs_version": (c.c_char_p, []),
         "lrs_check_device": (i32, []),
@@ -53,16 +75,12 @@ def _declare(L):
         "lrs_ista_alpha_workspace": (sz, [i64, i64, i64]),
         "lrs_ista_alpha_f32": (i32, [vp, i64, i64, vp, i64, i64, i32, f32, vp, vp, vp, sz, vp]),
         "lrs_ista_workspace": (sz, [i64, i64, i32]),
-        "lrs_ista_f32": (i32, [vp, vp, vp, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp, vp, sz, vp]),
-        "lrs_ista_set_rs_cols": (i32, [i32]),
+        "lrs_ista_f32": (i32, [vp, vp, vp, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp, c.POINTER(IstaOpts), vp,
+                               sz, vp]),
         "lrs_nlm_matlab_col_f32": (i32, [vp, i64, vp, i64, i64, i64, f64, vp, vp]),
         "lrs_ssim_f32": (i32, [vp, vp, i32, i32, i32, vp, vp]),
         "lrs_psnr_workspace": (sz, [i64, i64]),
         "lrs_psnr_bands_f32": (i32, [vp, vp, i64, i64, vp, vp, sz, vp]),
-        "lrs_ista_set_precision": (i32, [i32]),
-        "lrs_ista_get_precision": (i32, []),
-        "lrs_dip_set_precision": (i32, [i32]),
-        "lrs_dip_get_precision": (i32, []),
         "lrs_svt_workspace": (sz, [i64, i64]),
         "lrs_svt_f32": (i32, [vp, vp, f32, i64, i64, f64, vp, vp, i32, vp, sz, vp]),
         "lrs_svt_gram_f32": (i32, [vp, vp, f32, i64, i64, i32, vp, sz, vp]),
@@ -74,12 +92,13 @@ def _declare(L):
         # DIP low-rank prox
         "lrs_conv2d_out_size": (i32, [i32, i32, i32, i32, i32, i32, c.POINTER(c.c_int), c.POINTER(c.c_int)]),
         "lrs_conv2d_col_size": (i64, [i32, i32, i32, i32, i32, i32, i32]),
-        "lrs_conv2d_workspace": (sz, [i32, i32, i32, i32, i32, i32, i32, i32]),
-        "lrs_conv2d_fwd_f32": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, sz, vp]),
-        "lrs_conv2d_bwd_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, sz,
+        "lrs_conv2d_workspace": (sz, [i32, i32, i32, i32, i32, i32, i32, i32, dop]),
+        "lrs_conv2d_fwd_f32": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, dop, vp, sz,
                                      vp]),
-        "lrs_conv2d_bwd_x_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, sz,
-                                       vp]),
+        "lrs_conv2d_bwd_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, dop, vp,
+                                     sz, vp]),
+        "lrs_conv2d_bwd_x_f32": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, dop, vp,
+                                       sz, vp]),
         "lrs_bn_act_workspace": (sz, [i32, i64]),
         "lrs_bn_act_fwd_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, f32, f32, vp, sz, vp]),
         "lrs_bn_act_bwd_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, vp, sz, vp]),
@@ -93,7 +112,8 @@ def _declare(L):
         "lrs_image_to_unfolded_f32": (i32, [vp, i64, i64, i64, vp, vp]),
         "lrs_es_init": (i32, [vp, i32, i32, vp]),
         "lrs_es_update_f32": (i32, [vp, i64, vp, vp, vp]),
-        "lrs_dipnet_create": (i32, [vp, i32, i32, i32, i32, c.POINTER(vp)]),
+        "lrs_dipnet_create": (i32, [vp, i32, i32, i32, i32, dop, c.POINTER(vp)]),
+        "lrs_dipnet_get_opts": (i32, [vp, dop]),
         "lrs_dipnet_node_shape": (i32, [vp, i32, c.POINTER(c.c_int), c.POINTER(c.c_int), c.POINTER(c.c_int)]),
         "lrs_dipnet_destroy": (None, [vp]),
         "lrs_dipnet_num_params": (i64, [vp]),
@@ -107,7 +127,6 @@ def _declare(L):
         "lrs_dipnet_reset_optimizer": (i32, [vp, vp]),
         "lrs_dipnet_forward": (i32, [vp, vp, vp]),
         "lrs_dipnet_backward": (i32, [vp, vp, vp, vp]),
-        "lrs_dip_set_upsample_dgrad": (i32, [i32]),
         "lrs_dipnet_set_ln_lambda": (i32, [vp, f32]),
         "lrs_dipnet_output": (c.c_size_t, [vp]),
         "lrs_dipnet_grads": (c.c_size_t, [vp]),

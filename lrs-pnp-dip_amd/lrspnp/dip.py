@@ -141,16 +141,20 @@ def _check(rc, what):
 class DipNet:
     """A sequential conv net on the HIP engine (lrs_dipnet_*), with flat parameter buffers."""
 
-    def __init__(self, nodes: list[DipNode], C: int, H: int, W: int, device="cuda", params=None, bnstats=None):
+    def __init__(self, nodes: list[DipNode], C: int, H: int, W: int, device="cuda", params=None, bnstats=None,
+                 precision: int = _lib.DIP_SPLIT_BF16, upsample_dgrad: int = 0):
         """params / bnstats (optional): existing flat device buffers to bind (shared with another
-        engine of the same nodes at another H x W: the parameter layout does not depend on it)."""
+        engine of the same nodes at another H x W: the parameter layout does not depend on it).
+        precision / upsample_dgrad: this net's lrs_dip_opts, fixed at creation."""
         import torch
 
         self.L = _lib.device_lib()
         self.units = self.nodes = list(nodes)
         arr = (DipNode * len(nodes))(*nodes)
         h = ctypes.c_void_p()
-        _check(self.L.lrs_dipnet_create(arr, len(nodes), C, H, W, ctypes.byref(h)), "lrs_dipnet_create")
+        self.opts = _lib.dip_opts(precision, upsample_dgrad)
+        _check(self.L.lrs_dipnet_create(arr, len(nodes), C, H, W, ctypes.byref(self.opts), ctypes.byref(h)),
+               "lrs_dipnet_create")
         self.h = h
         self.H, self.W = H, W
         self.n_params = int(self.L.lrs_dipnet_num_params(h))

@@ -156,14 +156,25 @@ def slab_solver(Y, M, D, cfg, ctx: Ctx, device="cuda"):
 
 def gather_rows(X: torch.Tensor, ctx: Ctx):
     """The whole unfolded matrix from the ranks' row slabs, on rank 0 (numpy; None elsewhere).
-    Outside any timed region (object gather through host memory)."""
-    x = X.detach().cpu().numpy()
-    if not ctx.distributed:
-        return x
+    Outside any timed region.  A tensor gather (slabs padded to the largest, sizes exchanged
+    first): RCCL on the device under nccl, host tensors under gloo; no pickling."""
     import numpy as np
-    out = [None] * ctx.world
-    dist.all_gather_object(out, x)
-    return np.concatenate(out, axis=0) if ctx.rank == 0 else None
+    if not ctx.distributed:
+        return X.detach().cpu().numpy()
+    nccl = dist.get_backend() == "nccl"
+    dev = X.device if nccl else torch.device("cpu")
+    rows = torch.tensor([X.shape[0]], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(rows) for _ in range(ctx.world)]
+    dist.all_gather(sizes, rows)
+    sizes = [int(v.item()) for v in sizes]
+    mx = max(sizes)
+    mine = torch.zeros((mx,) + tuple(X.shape[1:]), dtype=X.dtype, device=dev)
+    mine[: X.shape[0]].copy_(X.detach())
+    parts = [torch.empty_like(mine) for _ in range(ctx.world)] if ctx.rank == 0 else None
+    dist.gather(mine, parts, dst=0)
+    if ctx.rank != 0:
+        return None
+    return np.concatenate([p[:n].cpu().numpy() for p, n in zip(parts, sizes)], axis=0)
 
 
 # ---- one cube, task-parallel DIP (SURVEY.md §8e, "DIP on GPU 0, sparse coding sharded over the rest") --
@@ -182,7 +193,9 @@ class DipTaskSplit:
         if cfg.lowrank != "dip":
             raise ValueError("DipTaskSplit needs a DIP configuration (LrsPnPConfig.dip_1lip / dip_pro)")
         self.ctx = ctx
-        self.s = LrsPnP(Y, M, D, cfg, device=device, image_shape=image_shape)
+        # only rank 0 trains the DIP: the workers keep the cube state but build no network engine
+        self.s = LrsPnP(Y, M, D, cfg, device=device, image_shape=image_shape,
+                        dip_engine=ctx.rank == 0 or ctx.world == 1)
         nb, W = self.s.nb, ctx.world
         self.ranges = [(0, 0)] * W
         if W > 1:
@@ -193,51 +206,64 @@ class DipTaskSplit:
                 self.ranges[r] = (b, b + c)
                 b += c
         self.maxc = max(b1 - b0 for b0, b1 in self.ranges) if W > 1 else nb
+        n_pad = self.s.phi.shape[1]
+        self.mine = torch.zeros((self.maxc, n_pad), dtype=torch.float32, device=self.s.phi.device)
         self.buf = None
+        self.comm_stream = torch.cuda.Stream(device=self.s.phi.device) if W > 1 else None
 
-    def _exchange(self, stream):
+    def _gather_phi(self, comm):
+        """The workers' Phi rows to every rank.  Under nccl it is enqueued on the comm stream as soon
+        as this rank's rows exist, so on rank 0 it runs beside the DIP training."""
         s, ctx = self.s, self.ctx
-        nccl = dist.get_backend() == "nccl"
-        if nccl:
-            with torch.cuda.stream(stream):
+        b0, b1 = self.ranges[ctx.rank]
+        n_pad = s.phi.shape[1]
+        if dist.get_backend() == "nccl":
+            if self.buf is None:
+                self.buf = torch.empty((ctx.world * self.maxc, n_pad), dtype=torch.float32, device=s.phi.device)
+            with torch.cuda.stream(comm):
+                if b1 > b0:
+                    self.mine[: b1 - b0].copy_(s.phi[b0:b1])
+                dist.all_gather_into_tensor(self.buf, self.mine)
+            return self.buf.view(ctx.world, self.maxc, n_pad)
+        comm.synchronize()
+        if b1 > b0:
+            self.mine[: b1 - b0].copy_(s.phi[b0:b1])
+        hs = [torch.empty((self.maxc, n_pad), dtype=torch.float32) for _ in range(ctx.world)]
+        dist.all_gather(hs, self.mine.cpu())
+        return hs
+
+    def _broadcast_u(self, comm):
+        s = self.s
+        if dist.get_backend() == "nccl":
+            with torch.cuda.stream(comm):
                 dist.broadcast(s.U, src=0)
         else:
-            stream.synchronize()
+            comm.synchronize()
             h = s.U.cpu()
             dist.broadcast(h, src=0)
             s.U.copy_(h)
-        n_pad = s.phi.shape[1]
-        b0, b1 = self.ranges[ctx.rank]
-        mine = torch.zeros((self.maxc, n_pad), dtype=torch.float32, device=s.phi.device)
-        if b1 > b0:
-            mine[: b1 - b0].copy_(s.phi[b0:b1])
-        if nccl:
-            if self.buf is None:
-                self.buf = torch.empty((ctx.world * self.maxc, n_pad), dtype=torch.float32, device=s.phi.device)
-            with torch.cuda.stream(stream):
-                dist.all_gather_into_tensor(self.buf, mine)
-            parts = self.buf.view(ctx.world, self.maxc, n_pad)
-        else:
-            stream.synchronize()
-            hs = [torch.empty((self.maxc, n_pad), dtype=torch.float32) for _ in range(ctx.world)]
-            dist.all_gather(hs, mine.cpu())
-            parts = hs
-        for r, (c0, c1) in enumerate(self.ranges):
-            if c1 > c0:
-                s.phi[c0:c1].copy_(parts[r][: c1 - c0], non_blocking=True)
 
     def step(self):
         s, ctx = self.s, self.ctx
         main = torch.cuda.current_stream()
         if ctx.world == 1:
             return s.step()
+        comm = self.comm_stream
         if ctx.rank == 0:
             lr = s.lowrank_stream
             lr.wait_stream(main)
+            comm.wait_stream(main)
+            parts = self._gather_phi(comm)        # beside the DIP (nccl): rank 0 contributes no rows
             s.low_rank_dip(lr)
-            main.wait_stream(lr)
+            comm.wait_stream(lr)
         else:
             b0, b1 = self.ranges[ctx.rank]
             s.sparse_coding_range(b0, b1, stream=main)
-        self._exchange(main)
+            comm.wait_stream(main)
+            parts = self._gather_phi(comm)
+        self._broadcast_u(comm)
+        main.wait_stream(comm)
+        for r, (c0, c1) in enumerate(self.ranges):
+            if c1 > c0:
+                s.phi[c0:c1].copy_(parts[r][: c1 - c0], non_blocking=True)
         s.admm(main)

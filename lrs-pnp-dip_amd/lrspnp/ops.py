@@ -10,6 +10,7 @@ import ctypes
 import numpy as np
 import torch
 
+from . import _lib as _libmod
 from ._lib import (ALPHA_FRO4, ALPHA_SOFT, ALPHA_SPEC2, PROX_NLM, PROX_NLM_MATLAB, PROX_SOFT, LrsError, check,
                    device_lib, lib)
 
@@ -125,9 +126,10 @@ def ista_workspace(n: int, K: int, prox: int, device) -> torch.Tensor | None:
 
 
 def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=None, coefs=None,
-         want_coefs=False, ws=None, stream=None):
+         want_coefs=False, ws=None, stream=None, precision: int | None = None):
     """Masked ISTA + prox over all blocks; returns phi (nb, n_pad) [, coefs (nb, K)].  `ws`: an
-    ista_workspace() buffer (allocated here when None and needed)."""
+    ista_workspace() buffer (allocated here when None and needed).  precision: this call's
+    lrs_ista_opts.precision (None = the library default, split-bf16)."""
     L = device_lib()
     _dev(Yb, torch.float32, "Yb")
     _dev(obs, torch.uint8, "obs")
@@ -142,8 +144,9 @@ def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=Non
         coefs = torch.empty((nb, K), dtype=torch.float32, device=Yb.device)
     if ws is None:
         ws = ista_workspace(n, K, prox, Yb.device)
+    opts = None if precision is None else ctypes.byref(_libmod.ista_opts(int(precision)))
     check(L.lrs_ista_f32(_p(Yb), _p(obs), _p(D), n, n_pad, K, nb, _p(alpha), _p(thr), int(Nit), int(prox),
-                         _p(coefs) if want_coefs else None, _p(phi), _p(ws), 0 if ws is None else ws.numel(),
+                         _p(coefs) if want_coefs else None, _p(phi), opts, _p(ws), 0 if ws is None else ws.numel(),
                          _s(stream)), "lrs_ista_f32")
     return (phi, coefs) if want_coefs else phi
 

@@ -72,7 +72,11 @@ class LrsPnP:
     dictionary with n = bb*bb.  All float32 (numpy or torch); copied to the device once.
     """
 
-    def __init__(self, Y, M, D, cfg: LrsPnPConfig | None = None, device="cuda", image_shape=None, comm=None):
+    def __init__(self, Y, M, D, cfg: LrsPnPConfig | None = None, device="cuda", image_shape=None, comm=None,
+                 dip_engine: bool = True):
+        """dip_engine=False (lowrank='dip' only): keep the DIP's target / mask / U buffers but build
+        no network engine -- a task-parallel worker rank that never trains the DIP
+        (lrspnp.dist.DipTaskSplit)."""
         self.cfg = cfg = cfg or LrsPnPConfig()
         # comm: None (whole cube here) or a row-slab communicator (lrspnp.dist.SlabComm): Y, M are
         # then this rank's pixel-row slab and the SVT Gram / convergence sums are all-reduced
@@ -141,11 +145,11 @@ class LrsPnP:
             self.svt_ws = ops.svt_workspace(self.P, self.B, dev)
             self.gram = ops.svt_gram_view(self.svt_ws, self.P, self.B) if comm is not None else None
         elif cfg.lowrank == "dip":
-            self._init_dip(image_shape, dev)
+            self._init_dip(image_shape, dev, engine=dip_engine)
         else:
             raise LrsError(f"unknown lowrank prox {cfg.lowrank!r}")
 
-    def _init_dip(self, image_shape, dev):
+    def _init_dip(self, image_shape, dev, engine=True):
         """DIP target = the observed cube as an image, mask_bkg = the pixel mask
         (…1-LiP.py:275-301); the network is re-initialised every outer iteration (:214)."""
         from .dip import DipConfig, LipschitzDip
@@ -155,7 +159,7 @@ class LrsPnP:
         if H * W != self.P:
             raise LrsError(f"image_shape {H}x{W} does not match P = {self.P}")
         self.H, self.W = H, W
-        self.dip = LipschitzDip(self.B, H, W, self.cfg.dip or DipConfig(), device=dev)
+        self.dip = LipschitzDip(self.B, H, W, self.cfg.dip or DipConfig(), device=dev) if engine else None
         self.dip_target = torch.empty((self.B, H, W), dtype=torch.float32, device=dev)
         ops.unfolded_to_image(self.Y, None, 1.0, H, W, self.dip_target)
         pix = ops.unfolded_to_image(self.M[:, :1].contiguous(), None, 1.0, H, W)   # (1, H, W)
@@ -204,7 +208,9 @@ class LrsPnP:
     def step(self):
         """One outer ADMM iteration (main_LRS_PnP.py:250-366), stream-ordered.  No host sync in
         the SVT mode; the DIP mode polls its early-stopping flag on the low-rank stream only."""
-        if self.dip is not None:
+        if self.cfg.lowrank == "dip":
+            if self.dip is None:
+                raise LrsError("this LrsPnP was built without a DIP engine (dip_engine=False)")
             return self._step_dip()
         main = torch.cuda.current_stream()
         lr = self.lowrank_stream

@@ -26,6 +26,26 @@ def test_library_exports_header_symbols():
     assert _lib.lib().lrs_version().startswith(b"lrspnp-hip")
 
 
+def test_no_process_wide_mode():
+    """reentrant, no global mutable state.  Every mode is a per-call option
+    (lrs_ista_opts, lrs_dip_opts) or fixed per handle; the only setter takes a lrs_dipnet; the
+    product library reads no environment variable (A/B knobs exist only in the tuning build)."""
+    src = open(os.path.join(REPO, "include", "lrspnp.h")).read()
+    setters = re.findall(r"int\s+(lrs_[a-z0-9_]*set_[a-z0-9_]*)\s*\(([^)]*)\)", src)
+    assert setters, "expected the per-handle lrs_dipnet_set_ln_lambda"
+    for name, args in setters:
+        assert args.strip().startswith("lrs_dipnet *net"), name
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for gone in ("lrs_dip_set_precision", "lrs_dip_get_precision", "lrs_dip_set_upsample_dgrad",
+                 "lrs_ista_set_precision", "lrs_ista_get_precision", "lrs_ista_set_rs_cols"):
+        assert not hasattr(L, gone), gone
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    und = subprocess.run([nm, "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert not re.search(r"\bgetenv\b", und), "the product library must not read the environment"
+
+
 def test_block_grid_matches_oracle():
     from lrspnp import ops
     for (P, B, bb, s) in [(1296, 128, 36, 36), (40000, 198, 8, 8), (262144, 224, 36, 36), (103, 29, 7, 7),
@@ -49,5 +69,6 @@ def test_cover_ranges():
 def test_invalid_arguments_rejected():
     L = _lib.lib()
     assert L.lrs_block_count(10, 10, 20, 20) < 0
-    assert L.lrs_ista_f32(None, None, None, 64, 64, 256, 10, None, None, 10, 0, None, None, None, 0, None) == -1
+    assert L.lrs_ista_f32(None, None, None, 64, 64, 256, 10, None, None, 10, 0, None, None, None, None, 0,
+                          None) == -1
     assert L.lrs_nlm_col_f32(None, 0, None, 0, 0, 0, 0.0, None, 3, 3, None) == -1

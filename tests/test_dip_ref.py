@@ -94,7 +94,7 @@ def test_engine_layout_matches_restatement():
 def _check_layout(L, units, c0, H):
     arr = (DipNode * len(units))(*units)
     h = ctypes.c_void_p()
-    assert L.lrs_dipnet_create(arr, len(units), c0, H, H, ctypes.byref(h)) == 0
+    assert L.lrs_dipnet_create(arr, len(units), c0, H, H, None, ctypes.byref(h)) == 0
     try:
         offs, n = dip_ref.param_offsets(units, c0, H, H)
         assert L.lrs_dipnet_num_params(h) == n

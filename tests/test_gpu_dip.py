@@ -19,6 +19,7 @@ import torch.nn.functional as F  # noqa: E402
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
 import dip_ref  # noqa: E402
+from lrspnp import _lib  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -77,17 +78,16 @@ def torch_conv(x, w, b, k, stride, pad, pad_mode, up):
 
 @pytest.fixture(params=["split_bf16", "f32"])
 def precision(request, L):
-    # LRS_DIP_SPLIT_BF16 = 1 (default), LRS_DIP_F32 = 0: arithmetic of the 128x128 GEMM tiles
-    old = L.lrs_dip_get_precision()
-    assert L.lrs_dip_set_precision(1 if request.param == "split_bf16" else 0) == 0
-    yield request.param
-    L.lrs_dip_set_precision(old)
+    # lrs_dip_opts.precision per call: LRS_DIP_SPLIT_BF16 = 1 (default), LRS_DIP_F32 = 0
+    return ctypes.byref(_lib.dip_opts(1 if request.param == "split_bf16" else 0))
 
 
-def test_dip_precision_switch(L):
-    assert L.lrs_dip_get_precision() == 1          # split-bf16 by default
-    assert L.lrs_dip_set_precision(7) != 0
-    assert L.lrs_dip_get_precision() == 1
+def test_dip_opts_rejects_bad_precision(L):
+    o = _lib.dip_opts(7)
+    assert L.lrs_conv2d_workspace(8, 8, 8, 8, 3, 1, 1, 0, ctypes.byref(o)) == 0
+    x = torch.zeros(8, 8, 8, device="cuda")
+    assert L.lrs_conv2d_fwd_f32(P(x), 8, 8, 8, P(x), None, 8, 3, 1, 1, 1, 0, None, P(x), ctypes.byref(o),
+                                None, 0, S()) == -1
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -105,17 +105,17 @@ def test_conv_fwd_bwd(L, case, precision):
     xd, wd, bd, gyd = (t.cuda().contiguous() for t in (x, w, b, gy))
     ncol = L.lrs_conv2d_col_size(cin, H, W, k, stride, pad, up)
     col = torch.empty(max(ncol, 1), device="cuda")
-    nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, stride, pad, up)
+    nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, stride, pad, up, precision)
     ws = torch.empty(nws // 4 + 1, device="cuda")
     y = torch.empty(cout, Ho, Wo, device="cuda")
     assert L.lrs_conv2d_fwd_f32(P(xd), cin, H, W, P(wd), P(bd), cout, k, stride, pad, pm, up,
-                                P(col) if ncol else None, P(y), P(ws), nws, S()) == 0
+                                P(col) if ncol else None, P(y), precision, P(ws), nws, S()) == 0
     assert rel(y, yr.detach()) < 1e-5
     div = torch.tensor([1.7], device="cuda")
     gw = torch.empty_like(wd)
     gx = torch.empty_like(xd)
     assert L.lrs_conv2d_bwd_f32(P(gyd), P(col) if ncol else P(xd), P(wd), P(div), cin, H, W, cout, k, stride,
-                                pad, pm, up, P(gx), P(gw), P(ws), nws, S()) == 0
+                                pad, pm, up, P(gx), P(gw), precision, P(ws), nws, S()) == 0
     torch.cuda.synchronize()
     assert rel(gw, wr.grad / 1.7) < 2e-5
     assert rel(gx, xr.grad) < 2e-5
@@ -123,9 +123,8 @@ def test_conv_fwd_bwd(L, case, precision):
 
 @pytest.fixture(params=[0, 1], ids=["fold", "upeff"])
 def upsample_dgrad(L, request):
-    assert L.lrs_dip_set_upsample_dgrad(request.param) == 0
-    yield request.param
-    L.lrs_dip_set_upsample_dgrad(0)
+    # lrs_dip_opts.upsample_dgrad, per call / per net
+    return request.param
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -142,17 +141,18 @@ def test_conv_implicit_fwd_bwd(L, case, upsample_dgrad):
     gy = torch.randn(yr.shape, generator=g)
     yr.backward(gy)
     xd, wd, bd, gyd = (t.cuda().contiguous() for t in (x, w, b, gy))
-    nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, stride, pad, up)
+    opts = ctypes.byref(_lib.dip_opts(1, upsample_dgrad))
+    nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, stride, pad, up, opts)
     ws = torch.empty(nws // 4 + 1, device="cuda")
     y = torch.full(yr.shape, float("nan"), device="cuda")
     assert L.lrs_conv2d_fwd_f32(P(xd), cin, H, W, P(wd), P(bd), cout, k, stride, pad, pm, up,
-                                None, P(y), P(ws), nws, S()) == 0
+                                None, P(y), opts, P(ws), nws, S()) == 0
     assert rel(y, yr.detach()) < 1e-5
     div = torch.tensor([1.7], device="cuda")
     gw = torch.full_like(wd, float("nan"))
     gx = torch.full_like(xd, float("nan"))
     assert L.lrs_conv2d_bwd_x_f32(P(gyd), P(xd), P(wd), P(div), cin, H, W, cout, k, stride,
-                                  pad, pm, up, P(gx), P(gw), P(ws), nws, S()) == 0
+                                  pad, pm, up, P(gx), P(gw), opts, P(ws), nws, S()) == 0
     torch.cuda.synchronize()
     assert rel(gw, wr.grad / 1.7) < 2e-5
     assert rel(gx, xr.grad) < 2e-5
@@ -308,9 +308,9 @@ def _problem(gold_seed=1234, units=None):
     return units, flat, x, t, m
 
 
-def _engine(units, flat, H=36, W=36, C=128):
+def _engine(units, flat, H=36, W=36, C=128, **opts):
     from lrspnp.dip import DipNet
-    net = DipNet(units, C, H, W)
+    net = DipNet(units, C, H, W, **opts)
     net.params.copy_(flat.cuda())
     net.reset_optimizer()
     return net
@@ -369,7 +369,7 @@ def test_unet_gradients_implicit_sizes_vs_fp64(L, upsample_dgrad):
     g = torch.Generator().manual_seed(5)
     x, t = torch.rand(128, H, H, generator=g), torch.rand(128, H, H, generator=g)
     m = (torch.rand(H * H, generator=g) > 0.1).float()
-    net = _engine(units, flat, H, H)
+    net = _engine(units, flat, H, H, upsample_dgrad=upsample_dgrad)
     grads = {}
     for dt in (torch.float64, torch.float32):
         p = flat.to(dt).clone().requires_grad_(True)
@@ -388,6 +388,49 @@ def test_unet_gradients_implicit_sizes_vs_fp64(L, upsample_dgrad):
         assert rel(Wg, Wr) < max(1e-4, 2 * rel(W32, Wr)), (i, rel(Wg, Wr), rel(W32, Wr))
         if gg is not None:
             assert rel(gg, gr) < max(1e-4, 2 * rel(g32, gr)) and rel(beg, ber) < max(1e-4, 2 * rel(be32, ber)), i
+
+
+def test_nets_with_different_opts_coexist(L):
+    """Per-handle modes (lrs_dip_opts, fixed at creation; no process-wide state): a split-bf16 and an
+    f32 net, and a zero-padded U-Net (its upsampled convs take the effective-kernel data gradient
+    when upsample_dgrad = 1) created with both modes, all interleaved in one process.  Each keeps
+    its own arithmetic: step-0 gradients match the fp64 restatement, and re-running a net after the
+    others gives bitwise its first result."""
+    from gen_dip_golden import flat_params
+    from lrspnp.dip import lipschitz_unet_units
+    H = 36
+    cases = []
+    for pad, opts in [("reflection", dict(precision=1)), ("reflection", dict(precision=0)),
+                      ("zero", dict(upsample_dgrad=1)), ("zero", dict(upsample_dgrad=0))]:
+        units = lipschitz_unet_units(128, 128, 128, pad=pad)
+        flat = torch.from_numpy(flat_params(units, 31, 128, H, H))
+        cases.append((units, flat, _engine(units, flat, H, H, **opts), opts))
+    for units, flat, net, opts in cases:
+        o = _lib.DipOpts()
+        assert net.L.lrs_dipnet_get_opts(net.h, ctypes.byref(o)) == 0
+        assert (o.precision, o.upsample_dgrad) == (opts.get("precision", 1), opts.get("upsample_dgrad", 0))
+    g = torch.Generator().manual_seed(8)
+    x, t = torch.rand(128, H, H, generator=g), torch.rand(128, H, H, generator=g)
+    m = (torch.rand(H * H, generator=g) > 0.1).float()
+    first = []
+    for units, flat, net, _ in cases:          # one backward each, interleaved
+        net.params.copy_(flat.cuda())
+        net.reset_optimizer()
+        net.train_steps(x.cuda(), t.cuda(), m.cuda(), 1, use_graph=False)
+        torch.cuda.synchronize()
+        first.append(net.grads.clone())
+    for k, (units, flat, net, _) in enumerate(cases):
+        p = flat.double().clone().requires_grad_(True)
+        dip_ref.loss_fn(dip_ref.forward(p, units, x.double()), t.double(), m.double()).backward()
+        p32 = flat.clone().requires_grad_(True)
+        dip_ref.loss_fn(dip_ref.forward(p32, units, x), t, m).backward()
+        assert rel(first[k], p.grad) < max(1e-4, 2 * rel(p32.grad, p.grad)), k
+    for k, (units, flat, net, _) in enumerate(cases):   # again, after all the others ran
+        net.params.copy_(flat.cuda())
+        net.reset_optimizer()
+        net.train_steps(x.cuda(), t.cuda(), m.cuda(), 1, use_graph=False)
+        torch.cuda.synchronize()
+        assert torch.equal(net.grads, first[k]), k
 
 
 def test_unet_graph_replay_equals_eager(L):

@@ -292,16 +292,13 @@ def test_ista_both_product_precisions_match_oracle():
     al, th = alpha.cpu().numpy(), thr.cpu().numpy()
     coefs_o, phi_o = O.ista_batch(Yb, obs, D, al, th, 30)
     out = {}
-    try:
-        for prec in (0, 1):
-            assert L.lrs_ista_set_precision(prec) == 0
-            phi, coefs = ops.ista(Yd, od, Dd, n, alpha, thr, 30, ops.PROX_NLM, want_coefs=True)
-            torch.cuda.synchronize()
-            out[prec] = (phi.cpu().numpy()[:, :n], coefs.cpu().numpy())
-            assert rel(out[prec][0], phi_o) < 1e-5 and rel(out[prec][1], coefs_o) < 1e-5
-    finally:
-        L.lrs_ista_set_precision(1)
+    for prec in (0, 1, None):          # lrs_ista_opts.precision per call (None: default = split-bf16)
+        phi, coefs = ops.ista(Yd, od, Dd, n, alpha, thr, 30, ops.PROX_NLM, want_coefs=True, precision=prec)
+        torch.cuda.synchronize()
+        out[prec] = (phi.cpu().numpy()[:, :n], coefs.cpu().numpy())
+        assert rel(out[prec][0], phi_o) < 1e-5 and rel(out[prec][1], coefs_o) < 1e-5
     assert rel(out[1][0], out[0][0]) < 1e-6
+    assert np.array_equal(out[None][0], out[1][0])      # no process-wide mode: the default is per call
 
 
 def test_nlm_matlab_prox_bitexact(ops):

@@ -27,3 +27,26 @@ def test_shim_resolves_reference_imports(tmp_path):
                        text=True, env=env, timeout=120)
     assert p.returncode == 0, p.stderr
     assert p.stdout.split() == ["lrspnp.compat", "lrspnp.nn", "lrspnp.nn", "True", "models.unet", "['a1']"]
+
+
+def test_shim_keeps_real_skimage_submodules(tmp_path):
+    """With a scikit-image installed, only skimage.restoration.denoise_nl_means is replaced: the real
+    package, its other restoration functions and its other submodules stay importable."""
+    sk = tmp_path / "site" / "skimage"
+    (sk / "restoration").mkdir(parents=True)
+    (sk / "metrics").mkdir()
+    (sk / "__init__.py").write_text("REAL = True\n")
+    (sk / "restoration" / "__init__.py").write_text(
+        "def denoise_nl_means(*a, **k):\n    raise RuntimeError('real nlm')\n"
+        "def estimate_sigma(x):\n    return 'real-sigma'\n")
+    (sk / "metrics" / "__init__.py").write_text("def peak_signal_noise_ratio():\n    return 'real-psnr'\n")
+    (tmp_path / "script.py").write_text(
+        "import skimage\n"
+        "from skimage.restoration import denoise_nl_means, estimate_sigma\n"
+        "from skimage.metrics import peak_signal_noise_ratio\n"
+        "print(skimage.REAL, denoise_nl_means.__module__, estimate_sigma(0), peak_signal_noise_ratio())\n")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(REPO, "lrs-pnp-dip_amd"), str(tmp_path / "site")]))
+    p = subprocess.run([sys.executable, "-m", "lrspnp.shim", str(tmp_path / "script.py")], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.split() == ["True", "lrspnp.compat", "real-sigma", "real-psnr"]

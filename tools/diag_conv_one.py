@@ -20,7 +20,7 @@ w = torch.randn(cout, cin, k, k, device="cuda") * 0.05
 b = torch.zeros(cout, device="cuda")
 Ho, Wo = ctypes.c_int(), ctypes.c_int()
 L.lrs_conv2d_out_size(H, W, k, s, p, up, ctypes.byref(Ho), ctypes.byref(Wo))
-nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, s, p, up)
+nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, s, p, up, None)
 ws = torch.empty(nws // 4 + 1, device="cuda")
 y = torch.empty(cout, Ho.value, Wo.value, device="cuda")
 gy = torch.randn_like(y)
@@ -28,8 +28,8 @@ gx, gw = torch.empty_like(x), torch.empty_like(w)
 div = torch.ones(1, device="cuda")
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 for _ in range(reps):
-    assert L.lrs_conv2d_fwd_f32(P(x), cin, H, W, P(w), P(b), cout, k, s, p, 1, up, None, P(y), P(ws), nws, st) == 0
+    assert L.lrs_conv2d_fwd_f32(P(x), cin, H, W, P(w), P(b), cout, k, s, p, 1, up, None, P(y), None, P(ws), nws, st) == 0
     assert L.lrs_conv2d_bwd_x_f32(P(gy), P(x), P(w), P(div), cin, H, W, cout, k, s, p, 1, up,
-                                  P(gx), P(gw), P(ws), nws, st) == 0
+                                  P(gx), P(gw), None, P(ws), nws, st) == 0
 torch.cuda.synchronize()
 print("ok")

@@ -31,7 +31,7 @@ gx, gw = torch.empty_like(x), torch.empty_like(w)
 div = torch.ones(1, device="cuda")
 ncol = L.lrs_conv2d_col_size(cin, H, W, k, stride, pad, up)
 col = torch.empty(max(ncol, 1), device="cuda") if explicit else None
-nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, stride, pad, up)
+nws = L.lrs_conv2d_workspace(cin, H, W, cout, k, stride, pad, up, None)
 ws = torch.empty(nws // 4 + 1, device="cuda")
 s = torch.cuda.current_stream()
 
@@ -39,13 +39,13 @@ s = torch.cuda.current_stream()
 def run():
     if not bwd:
         rc = L.lrs_conv2d_fwd_f32(P(x), cin, H, W, P(w), P(b), cout, k, stride, pad, 1, up, P(col) if explicit and ncol else None,
-                                  P(y), P(ws), nws, ctypes.c_void_p(s.cuda_stream))
+                                  P(y), None, P(ws), nws, ctypes.c_void_p(s.cuda_stream))
     elif explicit:
         rc = L.lrs_conv2d_bwd_f32(P(gy), P(col) if ncol else P(x), P(w), P(div), cin, H, W, cout, k, stride, pad, 1, up,
-                                  P(gx), P(gw), P(ws), nws, ctypes.c_void_p(s.cuda_stream))
+                                  P(gx), P(gw), None, P(ws), nws, ctypes.c_void_p(s.cuda_stream))
     else:
         rc = L.lrs_conv2d_bwd_x_f32(P(gy), P(x), P(w), P(div), cin, H, W, cout, k, stride, pad, 1, up, P(gx), P(gw),
-                                    P(ws), nws, ctypes.c_void_p(s.cuda_stream))
+                                    None, P(ws), nws, ctypes.c_void_p(s.cuda_stream))
     assert rc == 0, rc
 
 

@@ -1,6 +1,6 @@
 """Time the fused ISTA kernel (lrs_ista_f32) on the benchmark workloads (HIP events on its stream).
 
-    python tools/time_ista.py [--reps 5] [--cols 1|2]
+    python tools/time_ista.py [--reps 5]
 
 Workloads: configs[2] sparse coding (196x196x198 cube, 36x36 blocks, Nit 100, fro4: 6,408 blocks),
 the native 36x36x128 image (144 blocks), configs[3] (512x512x224, 50,974 blocks), and the bb = 8
@@ -48,10 +48,8 @@ def run(name, H, W, B, bb, nit, variant, reps, K=256):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--cols", type=int, default=1)
     ap.add_argument("--only", default="")
     a = ap.parse_args()
-    _lib.device_lib().lrs_ista_set_rs_cols(a.cols)
     jobs = [("cfg2_196x196x198_bb36_fro4", 196, 196, 198, 36, 100, "fro4"),
             ("native_36x36x128_bb36_fro4", 36, 36, 128, 36, 100, "fro4"),
             ("cfg1_200x200x198_bb8_spec2", 200, 200, 198, 8, 80, "spec2"),
