@@ -317,6 +317,13 @@ int lrs_dipnet_backward(lrs_dipnet *net, const float *x, const float *gout, void
 int lrs_dipnet_set_ln_lambda(lrs_dipnet *net, float ln_lambda);
 const float *lrs_dipnet_output(const lrs_dipnet *net);
 const float *lrs_dipnet_grads(const lrs_dipnet *net);
+/* diagnostics: node i's buffers in the workspace after a forward / backward (NULL where absent):
+ * its output, its pre-BatchNorm z, dL/dz, dL/d(output) */
+#define LRS_BUF_OUT 0
+#define LRS_BUF_Z 1
+#define LRS_BUF_GZ 2
+#define LRS_BUF_GRAD 3
+const float *lrs_dipnet_node_buffer(const lrs_dipnet *net, int node, int which);
 /* nsteps training steps: forward, masked MSE, backward, Adam; es (nullable) gets every step's
  * forward output (ring: es->size * C*H*W floats).  use_graph != 0 captures one step into a
  * hipGraph (on first use, re-captured when any argument changes) and replays it. */

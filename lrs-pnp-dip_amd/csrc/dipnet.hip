@@ -1707,6 +1707,19 @@ extern "C" const float *lrs_dipnet_output(const lrs_dipnet *net) {
 
 extern "C" const float *lrs_dipnet_grads(const lrs_dipnet *net) { return net ? net->grads : nullptr; }
 
+// Diagnostics: a node's activation buffers in the bound workspace (node's output, its pre-BN z,
+// dL/dz, dL/d(output)); NULL where the node has none.  Valid until the next call on the net.
+extern "C" const float *lrs_dipnet_node_buffer(const lrs_dipnet *net, int node, int which) {
+    if (!net || !net->ws || node < 0 || node >= (int)net->nodes.size()) return nullptr;
+    const auto &N = net->nodes[node];
+    int64_t off = -1;
+    if (which == LRS_BUF_OUT) off = N.out_off;
+    else if (which == LRS_BUF_Z) off = N.z_off;
+    else if (which == LRS_BUF_GZ) off = N.gz_off;
+    else if (which == LRS_BUF_GRAD) off = N.grad_off;
+    return off >= 0 ? net->f(off) : nullptr;
+}
+
 // The side stream and its fork/join events are created on the first training call (outside any
 // capture), so that creating a net and querying its layout needs no device.
 static int ensure_side(lrs_dipnet *net) {

@@ -287,6 +287,22 @@ class DipNet:
         _check(rc, "lrs_dipnet_train_steps")
         torch.cuda.current_stream().wait_stream(self.stream)
 
+    def node_buffer(self, node: int, which: int = 0):
+        """A copy of node `node`'s workspace buffer (0 output, 1 pre-BN z, 2 dL/dz, 3 dL/d(output);
+        None where absent), shaped (C, H, W) -- diagnostics."""
+        import torch
+        ptr = int(self.L.lrs_dipnet_node_buffer(self.h, int(node), int(which)))
+        if not ptr:
+            return None
+        c, h, w = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self.L.lrs_dipnet_node_shape(self.h, int(node), ctypes.byref(c), ctypes.byref(h), ctypes.byref(w))
+        n = c.value * h.value * w.value
+        base = self.ws.data_ptr()
+        off = (ptr - base) // 4
+        assert 0 <= off and (ptr - base) % 4 == 0 and off + n <= self.ws.numel() // 4
+        torch.cuda.synchronize()
+        return self.ws.view(torch.float32)[off:off + n].clone().view(c.value, h.value, w.value)
+
     def last_loss(self) -> float:
         v = ctypes.c_double()
         _check(self.L.lrs_dipnet_last_loss(self.h, ctypes.byref(v), ctypes.c_void_p(self.stream.cuda_stream)),

@@ -412,19 +412,28 @@ def test_nets_with_different_opts_coexist(L):
     g = torch.Generator().manual_seed(8)
     x, t = torch.rand(128, H, H, generator=g), torch.rand(128, H, H, generator=g)
     m = (torch.rand(H * H, generator=g) > 0.1).float()
-    first = []
+    first, flips = [], []
     for units, flat, net, _ in cases:          # one backward each, interleaved
         net.params.copy_(flat.cuda())
         net.reset_optimizer()
         net.train_steps(x.cuda(), t.cuda(), m.cuda(), 1, use_graph=False)
         torch.cuda.synchronize()
         first.append(net.grads.clone())
+        # LeakyReLU branches of this forward vs the fp64 restatement's (see below)
+        _, acts = dip_ref.forward(flat.double(), units, x.double(), return_all=True)
+        flips.append(sum(int(((net.node_buffer(i, 0).cpu() > 0) != (acts[i][0] > 0)).sum())
+                         for i in range(len(units))))
     for k, (units, flat, net, _) in enumerate(cases):
         p = flat.double().clone().requires_grad_(True)
         dip_ref.loss_fn(dip_ref.forward(p, units, x.double()), t.double(), m.double()).backward()
         p32 = flat.clone().requires_grad_(True)
         dip_ref.loss_fn(dip_ref.forward(p32, units, x), t, m).backward()
-        assert rel(first[k], p.grad) < max(1e-4, 2 * rel(p32.grad, p.grad)), k
+        # A pre-activation within ~1e-7 of 0 can take the other LeakyReLU branch than in fp64 (the
+        # forward is ~1e-6 from fp64); one flipped pixel moves every upstream gradient by ~1e-3
+        # (tools/diag_scale.py: 1 flip at node 12 -> 7e-4 for this data with the reflection net).
+        # Without a flip the 1e-4 bound holds; with one, the loose bound only guards the mode.
+        tol = max(1e-4, 2 * rel(p32.grad, p.grad)) if flips[k] == 0 else 5e-3
+        assert rel(first[k], p.grad) < tol, (k, flips[k], rel(first[k], p.grad))
     for k, (units, flat, net, _) in enumerate(cases):   # again, after all the others ran
         net.params.copy_(flat.cuda())
         net.reset_optimizer()
