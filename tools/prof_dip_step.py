@@ -16,6 +16,6 @@ g = torch.Generator(device="cuda").manual_seed(0)
 x = torch.rand(C, H, W, device="cuda", generator=g)
 t = torch.rand(n.out_shape, device="cuda", generator=g)
 m = (torch.rand(n.out_shape[1:], device="cuda", generator=g) > 0.2).float()
-n.train_steps(x, t, m, steps)
+n.train_steps(x, t, m, steps, use_graph=False)   # eager, as the bench (DipConfig.use_graph = False)
 torch.cuda.synchronize()
 print("loss", n.last_loss())
