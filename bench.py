@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--dip-steps", type=int, default=100, help="DIP steps per outer iteration (ES off, §8d)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--ista-max-wg", type=int, default=None,
+                    help="workgroups of the sparse-coding kernel beside the DIP (default LrsPnPConfig's; 0 = unbounded)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group: nccl (= RCCL, one GPU per rank) or gloo (rehearsal: rank r on GPU "
@@ -279,7 +281,8 @@ def main_dip(args, ctx):
     split = args.split_cube
     Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=0 if split else ctx.rank)
     dcfg = DipConfig(num_iter=args.dip_steps, early_stop=False, net="skip" if pro else "unet1lip")
-    cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, Nit=nit, dip=dcfg)
+    extra = {} if args.ista_max_wg is None else {"ista_max_wg_dip": args.ista_max_wg}
+    cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, Nit=nit, dip=dcfg, **extra)
     task = D.DipTaskSplit(Y, M, Dct, cfg, ctx, image_shape=(H, W)) if split else None
     s = task.s if split else LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
     clean_d = torch.from_numpy(clean).cuda()

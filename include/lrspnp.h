@@ -90,24 +90,35 @@ int lrs_ista_alpha_f32(const float *D, int64_t n, int64_t K, const uint8_t *obs_
  * Yb, obs: [nb][n_pad]; D: n x K; alpha[nb], thr[nb].  x0 = 0; Nit iterations of
  *   g = x + D^T(obs .* (y - D x)) / alpha ;  x = prox(g)
  * then phi[j*n_pad + r] = (D x_j)[r] for r < n (all rows, the inpainting step).
- * coefs (nullable) receives x [nb][K].  Any n (n_pad % 16 == 0), 1 <= K <= 512, every prox.
+ * coefs (nullable) receives x [nb][K].  Any n (n_pad % 16 == 0), any K <= 16384 (K > 512 on the
+ * generic dense-GEMM path, see lrs_ista_opts), every prox.
  * n_pad <= 64 with K = 256 runs the dictionary-resident kernels (ws unused); everything else runs
  * the row-split kernel, whose fragment-ordered dictionary images live in `ws`
  * (lrs_ista_workspace bytes; LRS_E_WORKSPACE when too small).
  * Replaces the per-block loop of main_LRS_PnP.py:270-303 / main_LRS_PnP_DIP_1-LiP.py:367-392
  * around ista() (main_LRS_PnP.py:131-149, …1-LiP.py:185-198) and delete_element (:201-204). */
-/* Per-call options (NULL = defaults).  precision: arithmetic of the two products of the resident
- * (n_pad <= 64) kernel: LRS_ISTA_SPLIT_BF16 (default): bf16 matrix cores on operands split exactly
- * into three bf16 terms (six partial products, fp32 accumulation: fp32-GEMM accuracy, not bitwise
- * the f32 MFMA); LRS_ISTA_F32: v_mfma_f32_16x16x4_f32 (exact f32 products).  The NLM prox is
- * identical.  The library keeps no process-wide mode. */
+/* Per-call options (NULL = defaults); the library keeps no process-wide mode.
+ *   precision: arithmetic of the two products of the resident (n_pad <= 64) kernel:
+ *     LRS_ISTA_SPLIT_BF16 (default): bf16 matrix cores on operands split exactly into three bf16
+ *     terms (six partial products, fp32 accumulation: fp32-GEMM accuracy, not bitwise the f32
+ *     MFMA); LRS_ISTA_F32: v_mfma_f32_16x16x4_f32 (exact f32 products).  The NLM prox is identical.
+ *   max_workgroups: 0 (default) = one workgroup per 16-block tile; > 0 bounds the row-split
+ *     kernel's grid (each workgroup then loops over tiles), so a concurrent launch on another
+ *     stream (the DIP training of the …_DIP mains) keeps the rest of the CUs.  Results do not
+ *     depend on it. */
 #define LRS_ISTA_F32 0
 #define LRS_ISTA_SPLIT_BF16 1
+#define LRS_ISTA_ALGO_AUTO 0
+#define LRS_ISTA_ALGO_GENERIC 1
 typedef struct {
     int32_t precision;
-    int32_t reserved[7];
+    int32_t max_workgroups;
+    int32_t algorithm;    /* LRS_ISTA_ALGO_AUTO: the fused kernels for K <= 512, the generic path above;
+                             LRS_ISTA_ALGO_GENERIC: every inner iteration as two dense fp32-accurate
+                             GEMMs + the prox kernel, chunks of 4096 blocks (any K <= 16384) */
+    int32_t reserved[5];
 } lrs_ista_opts;
-size_t lrs_ista_workspace(int64_t n, int64_t K, int prox);
+size_t lrs_ista_workspace(int64_t n, int64_t K, int prox, const lrs_ista_opts *opts);
 int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,
                  int64_t K, int64_t nb, const float *alpha, const double *thr, int Nit, int prox,
                  float *coefs, float *phi, const lrs_ista_opts *opts, void *ws, size_t ws_bytes,

@@ -807,6 +807,17 @@ __global__ void k_image_to_unfolded(const float *__restrict__ img, int64_t H, in
 
 }  // namespace
 
+// Dense fp32-accurate GEMM for the library's other components (the K > 512 ISTA path, ista.hip):
+// C[M][N] = op(A) op(B) with the DIP engine's split-bf16 / f32 kernels, split-K summed in fixed
+// order (deterministic).  part: >= dense_gemm_part_floats(M, N, K) floats.
+namespace lrs {
+int64_t dense_gemm_part_floats(int M, int N, int K) { return gemm_part_floats(M, N, K); }
+int dense_gemm(int TA, int TB, const float *A, const float *B, float *C, int M, int N, int K, float *part,
+               int64_t part_cap, hipStream_t st) {
+    return gemm(LRS_DIP_SPLIT_BF16, TA, TB, A, B, C, nullptr, nullptr, M, N, K, part, part_cap, st);
+}
+}  // namespace lrs
+
 // ============================================================================================
 // Primitive C ABI
 // ============================================================================================

@@ -18,6 +18,8 @@
 //    whole dictionary stays resident for the kernel's lifetime; larger n streams 64-row stages;
 //  * the NLM prox runs in fp64 on the accumulator layout: a lane holds 4 consecutive atoms per
 //    16-atom tile, the 3+4 neighbours it needs come from lanes l-16 / l+16 (ds_bpermute).
+#include <algorithm>
+
 #include "lrs_common.h"
 #include "lrs_nlm.h"
 
@@ -1211,9 +1213,116 @@ namespace lrs {
 size_t ista_rs_workspace(int64_t n, int64_t K);
 int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
                    const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi, void *ws,
-                   size_t ws_bytes, hipStream_t st);
+                   size_t ws_bytes, int64_t max_wg, hipStream_t st);
 int nlm_matlab_col_launch(const float *g, int64_t ldg, float *out, int64_t ldo, int64_t K, int64_t nvec, double h,
                           const double *h_per_vec, hipStream_t st);
+int64_t dense_gemm_part_floats(int M, int N, int K);
+int dense_gemm(int TA, int TB, const float *A, const float *B, float *C, int M, int N, int K, float *part,
+               int64_t part_cap, hipStream_t st);
+
+// ---- generic path (any K; the only one for K > 512): the iteration as dense GEMMs ----------------
+// Per chunk of up to kGenChunk blocks, every inner iteration is
+//   R = X D^T            (chunk x n, dense GEMM)       r = obs .* (Yb - R)
+//   G = r D              (chunk x K, dense GEMM)       g = X + G / alpha        X = prox(g)
+// and finally Phi = X D^T, the reference's per-block loop (main_LRS_PnP.py:270-303, ista() :131-149)
+// for all blocks of the chunk at once.  The products are fp32-accurate (split-bf16 or f32 MFMA),
+// the prox is the same kernel as lrs_nlm_col_f32 / lrs_nlm_matlab_col_f32.
+constexpr int64_t kGenChunk = 4096;
+
+__global__ void k_gen_resid(float *__restrict__ R, const float *__restrict__ Yb, const uint8_t *__restrict__ obs,
+                            int64_t rows, int n, int n_pad) {
+    const int64_t total = rows * n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = i / n;
+        const int r = (int)(i - j * n);
+        R[i] = obs[j * n_pad + r] ? Yb[j * n_pad + r] - R[i] : 0.0f;
+    }
+}
+
+// g = x + G / alpha (in place in G); the quotient as the oracle / reference ((H^T r) / alpha)
+__global__ void k_gen_grad(float *__restrict__ G, const float *__restrict__ X, const float *__restrict__ alpha,
+                           int64_t rows, int K) {
+    const int64_t total = rows * K;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = i / K;
+        G[i] = X[i] + G[i] / alpha[j];
+    }
+}
+
+__global__ void k_gen_soft(const float *__restrict__ G, float *__restrict__ X, const double *__restrict__ thr,
+                           int64_t rows, int K) {
+    const int64_t total = rows * K;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const float T = (float)thr[i / K], gv = G[i];
+        float t = fabsf(gv) - T;
+        t = t > 0.f ? t : 0.f;
+        X[i] = gv > 0.f ? t : (gv < 0.f ? -t : 0.f);
+    }
+}
+
+__global__ void k_gen_phi(const float *__restrict__ R, float *__restrict__ phi, int64_t rows, int n, int n_pad) {
+    const int64_t total = rows * n_pad;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = i / n_pad;
+        const int r = (int)(i - j * n_pad);
+        phi[i] = r < n ? R[j * n + r] : 0.0f;
+    }
+}
+
+inline unsigned gen_blocks(int64_t n) { return (unsigned)std::min<int64_t>((n + 255) / 256, 8192); }
+
+size_t ista_generic_workspace(int64_t n, int64_t K) {
+    const int64_t c = kGenChunk;
+    const int64_t part = std::max(dense_gemm_part_floats((int)c, (int)n, (int)K), dense_gemm_part_floats((int)c, (int)K, (int)n));
+    return (size_t)(2 * c * K + c * n + part) * sizeof(float) + 256;
+}
+
+int ista_generic(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
+                 const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi, void *ws,
+                 size_t ws_bytes, hipStream_t st) {
+    if (!ws || ws_bytes < ista_generic_workspace(n, K)) return LRS_E_WORKSPACE;
+    if (n > INT32_MAX / 2 || K > 16384) return LRS_E_UNSUPPORTED;
+    const int64_t c = kGenChunk;
+    float *X = (float *)ws, *G = X + c * K, *R = G + c * K, *part = R + c * n;
+    const int64_t part_cap = std::max(dense_gemm_part_floats((int)c, (int)n, (int)K),
+                                      dense_gemm_part_floats((int)c, (int)K, (int)n));
+    for (int64_t j0 = 0; j0 < nb; j0 += c) {
+        const int rows = (int)std::min(c, nb - j0);
+        hipError_t e = hipMemsetAsync(X, 0, sizeof(float) * rows * K, st);
+        if (e != hipSuccess) return (int)e;
+        for (int it = 0; it < Nit; ++it) {
+            int rc = dense_gemm(0, 1, X, D, R, rows, (int)n, (int)K, part, part_cap, st);   // R = X D^T
+            if (rc) return rc;
+            hipLaunchKernelGGL(k_gen_resid, dim3(gen_blocks(rows * n)), dim3(256), 0, st, R, Yb + j0 * n_pad,
+                               obs + j0 * n_pad, (int64_t)rows, (int)n, (int)n_pad);
+            rc = dense_gemm(0, 0, R, D, G, rows, (int)K, (int)n, part, part_cap, st);          // G = r D
+            if (rc) return rc;
+            hipLaunchKernelGGL(k_gen_grad, dim3(gen_blocks(rows * K)), dim3(256), 0, st, G, X, alpha + j0,
+                               (int64_t)rows, (int)K);
+            if (prox == LRS_PROX_SOFT) {
+                hipLaunchKernelGGL(k_gen_soft, dim3(gen_blocks(rows * K)), dim3(256), 0, st, G, X, thr + j0,
+                                   (int64_t)rows, (int)K);
+            } else if (prox == LRS_PROX_NLM_MATLAB) {
+                rc = nlm_matlab_col_launch(G, K, X, K, K, rows, 0.0, thr + j0, st);
+                if (rc) return rc;
+            } else {
+                hipLaunchKernelGGL(k_nlm_col, dim3((unsigned)rows), dim3(256), (size_t)(K + 10) * sizeof(float), st, G,
+                                   K, X, K, (int)K, 0.0, thr + j0);
+            }
+            LRS_CHECK_LAUNCH();
+        }
+        int rc = dense_gemm(0, 1, X, D, R, rows, (int)n, (int)K, part, part_cap, st);          // Phi = X D^T
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_gen_phi, dim3(gen_blocks(rows * n_pad)), dim3(256), 0, st, R, phi + j0 * n_pad,
+                           (int64_t)rows, (int)n, (int)n_pad);
+        if (coefs) {
+            e = hipMemcpyAsync(coefs + j0 * K, X, sizeof(float) * rows * K, hipMemcpyDeviceToDevice, st);
+            if (e != hipSuccess) return (int)e;
+        }
+        LRS_CHECK_LAUNCH();
+    }
+    return LRS_OK;
+}
 }  // namespace lrs
 
 // The resident kernels (dictionary in LDS) serve n_pad <= 64 with K = 256 and the skimage / soft
@@ -1222,8 +1331,14 @@ static bool ista_resident(int64_t n_pad, int64_t K, int prox) {
     return n_pad <= kStageRows && K == 256 && prox != LRS_PROX_NLM_MATLAB;
 }
 
-extern "C" size_t lrs_ista_workspace(int64_t n, int64_t K, int prox) {
+// the dense-GEMM path: K > 512, or asked for (lrs_ista_opts.algorithm)
+static bool ista_use_generic(int64_t K, const lrs_ista_opts *opts) {
+    return K > 512 || (opts && opts->algorithm == LRS_ISTA_ALGO_GENERIC);
+}
+
+extern "C" size_t lrs_ista_workspace(int64_t n, int64_t K, int prox, const lrs_ista_opts *opts) {
     if (n <= 0 || K <= 0) return 0;
+    if (ista_use_generic(K, opts)) return ista_generic_workspace(n, K);
     if (ista_resident(round_up(n, 16), K, prox)) return 0;
     return ista_rs_workspace(n, K);
 }
@@ -1235,14 +1350,18 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     if (!Yb || !obs || !D || !alpha || !thr || !phi || n <= 0 || nb < 0 || Nit < 0 || K <= 0) return LRS_E_INVALID;
     const int precision = opts ? opts->precision : LRS_ISTA_SPLIT_BF16;   // per call (no process state)
     if (precision != LRS_ISTA_F32 && precision != LRS_ISTA_SPLIT_BF16) return LRS_E_INVALID;
+    const int64_t max_wg = opts ? opts->max_workgroups : 0;
+    if (max_wg < 0) return LRS_E_INVALID;
+    if (opts && opts->algorithm != LRS_ISTA_ALGO_AUTO && opts->algorithm != LRS_ISTA_ALGO_GENERIC) return LRS_E_INVALID;
     if (n_pad % 16 != 0 || n_pad < n) return LRS_E_INVALID;
     if (prox != LRS_PROX_NLM && prox != LRS_PROX_SOFT && prox != LRS_PROX_NLM_MATLAB) return LRS_E_INVALID;
-    if (K > 512) return LRS_E_UNSUPPORTED;
     if (n_pad > (int64_t)1 << 20 || nb > ((int64_t)1 << 40)) return LRS_E_INVALID;
     if (nb == 0) return LRS_OK;
     hipStream_t st = (hipStream_t)stream;
+    if (ista_use_generic(K, opts))
+        return ista_generic(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, st);
     if (!ista_resident(n_pad, K, prox))
-        return ista_rs_launch(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, st);
+        return ista_rs_launch(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, max_wg, st);
     IstaParams p{Yb, obs, D, alpha, thr, coefs, phi, (int)n, (int)n_pad, Nit, prox, nb, 7.0};
     const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
     dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));

@@ -152,8 +152,13 @@ __global__ __launch_bounds__(256, MINW) void k_ista_rs(IstaRsParams p) {
     const int NT = p.n_pad >> 4;
     const int t0 = (NT * w) / S, t1 = (NT * (w + 1)) / S;
     const int K = p.K;
+    const int64_t ntiles = (p.nb + 15) / 16;
 
-    const int64_t j = (int64_t)blockIdx.x * 16 + jl;
+    // persistent over column tiles when the grid is bounded (lrs_ista_opts.max_workgroups): each
+    // tile is independent, so the results do not depend on the grid
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    if (tile != blockIdx.x) __syncthreads();   // the previous tile's last reads of xbuf / gbuf are done
+    const int64_t j = tile * 16 + jl;
     const bool valid = j < p.nb;
     const float al = valid ? p.alpha[j] : 1.0f;
     const float ral = 1.0f / al;
@@ -367,6 +372,7 @@ __global__ __launch_bounds__(256, MINW) void k_ista_rs(IstaRsParams p) {
             *reinterpret_cast<float4 *>(&p.phi[j * p.n_pad + 16 * t + 4 * g]) = make_float4(R[0], R[1], R[2], R[3]);
         }
     }
+    }   // tile
 }
 
 // Fragment-ordered dictionary images (zero past n rows / K atoms).  One thread per float4.
@@ -446,8 +452,9 @@ static int rs_pick_waves(int64_t tiles, int NT, int NQ, int minw) {
 }
 
 template <int NQ, int MINW, int S>
-static int launch_rs_k(const IstaRsParams &p, hipStream_t st) {
-    const int64_t tiles = (p.nb + 15) / 16;
+static int launch_rs_k(const IstaRsParams &p, int64_t max_wg, hipStream_t st) {
+    int64_t tiles = (p.nb + 15) / 16;
+    if (max_wg > 0 && tiles > max_wg) tiles = max_wg;
     static bool lds_opt_in = false;   // dynamic LDS beyond 64 KiB
     if (!lds_opt_in) {
         const hipError_t e = hipFuncSetAttribute((const void *)k_ista_rs<NQ, MINW, S>,
@@ -461,19 +468,19 @@ static int launch_rs_k(const IstaRsParams &p, hipStream_t st) {
 }
 
 template <int NQ, int MINW>
-static int launch_rs(const IstaRsParams &p, int NT, hipStream_t st) {
+static int launch_rs(const IstaRsParams &p, int NT, int64_t max_wg, hipStream_t st) {
     const int64_t tiles = (p.nb + 15) / 16;
     switch (rs_pick_waves(tiles, NT, NQ, MINW)) {
-    case 1: return launch_rs_k<NQ, MINW, 1>(p, st);
-    case 2: return launch_rs_k<NQ, MINW, 2>(p, st);
-    case 3: return launch_rs_k<NQ, MINW, 3>(p, st);
-    default: return launch_rs_k<NQ, MINW, 4>(p, st);
+    case 1: return launch_rs_k<NQ, MINW, 1>(p, max_wg, st);
+    case 2: return launch_rs_k<NQ, MINW, 2>(p, max_wg, st);
+    case 3: return launch_rs_k<NQ, MINW, 3>(p, max_wg, st);
+    default: return launch_rs_k<NQ, MINW, 4>(p, max_wg, st);
     }
 }
 
 int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
                    const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi, void *ws,
-                   size_t ws_bytes, hipStream_t st) {
+                   size_t ws_bytes, int64_t max_wg, hipStream_t st) {
     if (K < 1 || K > 512) return LRS_E_UNSUPPORTED;
     const int NQ = rs_nq(K);
     const int NT = (int)(n_pad / 16);
@@ -490,10 +497,10 @@ int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t 
     }
     IstaRsParams p{Yb, obs, DAf, DTf, alpha, thr, coefs, phi, (int)n_pad, (int)K, Nit, prox, nb, 7.0};
     switch (NQ) {
-    case 4: return launch_rs<4, 2>(p, NT, st);
-    case 8: return launch_rs<8, 2>(p, NT, st);
-    case 16: return launch_rs<16, 2>(p, NT, st);
-    default: return launch_rs<32, 1>(p, NT, st);
+    case 4: return launch_rs<4, 2>(p, NT, max_wg, st);
+    case 8: return launch_rs<8, 2>(p, NT, max_wg, st);
+    case 16: return launch_rs<16, 2>(p, NT, max_wg, st);
+    default: return launch_rs<32, 1>(p, NT, max_wg, st);
     }
 }
 

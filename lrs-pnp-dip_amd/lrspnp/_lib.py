@@ -29,16 +29,20 @@ ISTA_F32, ISTA_SPLIT_BF16 = 0, 1
 DIP_F32, DIP_SPLIT_BF16 = 0, 1
 
 
+ISTA_ALGO_AUTO, ISTA_ALGO_GENERIC = 0, 1
+
+
 class IstaOpts(ctypes.Structure):
-    _fields_ = [("precision", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+    _fields_ = [("precision", ctypes.c_int32), ("max_workgroups", ctypes.c_int32), ("algorithm", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 5)]
 
 
 class DipOpts(ctypes.Structure):
     _fields_ = [("precision", ctypes.c_int32), ("upsample_dgrad", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
 
 
-def ista_opts(precision: int = ISTA_SPLIT_BF16) -> IstaOpts:
-    return IstaOpts(precision=precision)
+def ista_opts(precision: int = ISTA_SPLIT_BF16, max_workgroups: int = 0, algorithm: int = ISTA_ALGO_AUTO) -> IstaOpts:
+    return IstaOpts(precision=precision, max_workgroups=max_workgroups, algorithm=algorithm)
 
 
 def dip_opts(precision: int = DIP_SPLIT_BF16, upsample_dgrad: int = 0) -> DipOpts:
@@ -74,7 +78,7 @@ def _declare(L):
         "lrs_im2col_f32": (i32, [vp, vp, f32, i64, i64, i64, vp, vp, i64, i64, vp, vp, vp]),
         "lrs_ista_alpha_workspace": (sz, [i64, i64, i64]),
         "lrs_ista_alpha_f32": (i32, [vp, i64, i64, vp, i64, i64, i32, f32, vp, vp, vp, sz, vp]),
-        "lrs_ista_workspace": (sz, [i64, i64, i32]),
+        "lrs_ista_workspace": (sz, [i64, i64, i32, c.POINTER(IstaOpts)]),
         "lrs_ista_f32": (i32, [vp, vp, vp, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp, c.POINTER(IstaOpts), vp,
                                sz, vp]),
         "lrs_nlm_matlab_col_f32": (i32, [vp, i64, vp, i64, i64, i64, f64, vp, vp]),

@@ -78,8 +78,8 @@ def delete_element(tensor, indices):
 def _ista(y, H, lambda_ista, Nit, mode, prox):
     Hn = _as_f32_cpu(H)
     m, K = Hn.shape
-    if K > 512:
-        raise LrsError(f"lrspnp's ISTA kernels take K <= 512 atoms, got {K}")
+    if K > 4096:       # the alpha kernel's LDS bound; K > 512 runs the generic dense-GEMM ISTA path
+        raise LrsError(f"lrspnp's ISTA takes K <= 4096 atoms, got {K}")
     yn = _as_f32_cpu(y).reshape(-1)
     if yn.size != m:
         raise ValueError(f"y has {yn.size} rows, H has {m}")

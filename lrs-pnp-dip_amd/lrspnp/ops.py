@@ -118,18 +118,22 @@ def ista_alpha(D, obs_pat, n: int, mode: int, lambda_ista: float, stream=None):
     return alpha, thr
 
 
-def ista_workspace(n: int, K: int, prox: int, device) -> torch.Tensor | None:
-    """Device workspace of lrs_ista_f32 (the row-split kernel's fragment-ordered dictionary images);
-    None when the dictionary-resident kernels serve (n <= 64, K = 256, skimage / soft prox)."""
-    nbytes = int(lib().lrs_ista_workspace(int(n), int(K), int(prox)))
+def ista_workspace(n: int, K: int, prox: int, device, algorithm: int = 0) -> torch.Tensor | None:
+    """Device workspace of lrs_ista_f32 (the row-split kernel's fragment-ordered dictionary images,
+    or the generic path's chunk buffers for K > 512); None when the dictionary-resident kernels serve
+    (n <= 64, K = 256, skimage / soft prox)."""
+    opts = ctypes.byref(_libmod.ista_opts(algorithm=int(algorithm))) if algorithm else None
+    nbytes = int(lib().lrs_ista_workspace(int(n), int(K), int(prox), opts))
     return torch.empty(nbytes, dtype=torch.uint8, device=device) if nbytes else None
 
 
 def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=None, coefs=None,
-         want_coefs=False, ws=None, stream=None, precision: int | None = None):
+         want_coefs=False, ws=None, stream=None, precision: int | None = None, max_workgroups: int = 0,
+         algorithm: int = 0):
     """Masked ISTA + prox over all blocks; returns phi (nb, n_pad) [, coefs (nb, K)].  `ws`: an
-    ista_workspace() buffer (allocated here when None and needed).  precision: this call's
-    lrs_ista_opts.precision (None = the library default, split-bf16)."""
+    ista_workspace() buffer (allocated here when None and needed).  precision / max_workgroups /
+    algorithm: this call's lrs_ista_opts (None / 0 = the library defaults; algorithm 1 = the generic
+    dense-GEMM path that K > 512 always takes)."""
     L = device_lib()
     _dev(Yb, torch.float32, "Yb")
     _dev(obs, torch.uint8, "obs")
@@ -143,8 +147,11 @@ def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=Non
     if want_coefs and coefs is None:
         coefs = torch.empty((nb, K), dtype=torch.float32, device=Yb.device)
     if ws is None:
-        ws = ista_workspace(n, K, prox, Yb.device)
-    opts = None if precision is None else ctypes.byref(_libmod.ista_opts(int(precision)))
+        ws = ista_workspace(n, K, prox, Yb.device, algorithm)
+    opts = None
+    if precision is not None or max_workgroups or algorithm:
+        opts = ctypes.byref(_libmod.ista_opts(_libmod.ISTA_SPLIT_BF16 if precision is None else int(precision),
+                                              int(max_workgroups), int(algorithm)))
     check(L.lrs_ista_f32(_p(Yb), _p(obs), _p(D), n, n_pad, K, nb, _p(alpha), _p(thr), int(Nit), int(prox),
                          _p(coefs) if want_coefs else None, _p(phi), opts, _p(ws), 0 if ws is None else ws.numel(),
                          _s(stream)), "lrs_ista_f32")

@@ -37,6 +37,11 @@ class LrsPnPConfig:
     lowrank: str = "svt"          # 'svt' (main_LRS_PnP.py:315) or 'dip' (…1-LiP.py:399-411)
     dip: object = None            # lrspnp.dip.DipConfig for lowrank='dip' (None: reference defaults)
     dip_seed: int = 0             # DIP init seed of outer iteration t is dip_seed + t
+    # Workgroups of the sparse-coding kernel beside the DIP training (lowrank='dip';
+    # lrs_ista_opts.max_workgroups, 0 = one per 16-block tile).  Measured at configs[2]
+    # (bench.py --ista-max-wg): 0 -> 7.25 outer it/s, 128 -> 7.18, 64 -> 6.97, 32 -> 6.68: a longer,
+    # narrower sparse coding taxes the DIP more than a short full-chip one, so unbounded.
+    ista_max_wg_dip: int = 0
 
     @staticmethod
     def dip_1lip(**kw) -> "LrsPnPConfig":
@@ -246,7 +251,7 @@ class LrsPnP:
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
                    stream=main)
         ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
-                 ws=self.ista_ws, stream=main)
+                 ws=self.ista_ws, stream=main, max_workgroups=self.cfg.ista_max_wg_dip)
         self.low_rank_dip(lr)
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,

@@ -1,0 +1,57 @@
+"""GPU: the DIP mains end to end against the reference's own runs (SURVEY.md §4 "Statistical E2E").
+
+tests/golden/dip_e2e_ref.npz holds the per-outer-iteration MPSNR / MSSIM of the unmodified
+main_LRS_PnP_DIP_1-LiP.py and main_LRS_PnP_DIP_pro.py on their own 36x36x128 data (early stopping
+on, as written) over 5 DIP-init seeds (tests/golden/gen_dip_e2e.py).  DIP training trajectories are
+not reproducible even by the reference (tests/test_dip_ref.py: 1 vs 3 CPU threads already differ),
+so the comparison is statistical: lrspnp.LrsPnP with the same data, dictionary and parameters over
+as many seeds of its own init RNG must give, per outer iteration, a mean inside the reference's
+min..max over seeds widened by 0.01 dB (north_star's PSNR tolerance); the same for MSSIM widened by
+0.005.  Measured (tools/e2e_dip_gpu.py): 1-Lip means 34.282 34.749 35.029 35.193 vs the
+reference's 34.286 34.747 35.011 35.189; pro 34.100 34.529 34.835 35.157 vs 34.067 34.543 34.859
+35.142.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lrspnp import _lib
+    return _lib.device_lib()
+
+
+@pytest.mark.parametrize("net", ["1lip", "pro"])
+def test_dip_main_quality_within_reference_band(gpu, golden, net):
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.data import mask_matrix, synthetic_dictionary, unfold
+    from lrspnp.metrics import fold, mpsnr, mssim
+    ref = golden("dip_e2e_ref.npz")
+    R, RS = ref[f"{net}_mpsnr"], ref[f"{net}_mssim"]          # (seeds, iterations)
+    nseed, iters = R.shape
+    d = golden("data_img5.npz")
+    Y, M = unfold(d["noisy"][0]), mask_matrix(d["lrs_mask"], 128)
+    D = synthetic_dictionary(1296, 256, 0)
+    clean = torch.from_numpy(d["clean"][0]).cuda()
+    mk = LrsPnPConfig.dip_1lip if net == "1lip" else LrsPnPConfig.dip_pro
+    G, GS = np.empty((nseed, iters)), np.empty((nseed, iters))
+    for seed in range(nseed):
+        s = LrsPnP(Y, M, D, mk(dip_seed=1000 * seed), image_shape=(36, 36))
+        for it in range(iters):
+            s.step()
+            G[seed, it] = mpsnr(s.X, clean)
+            GS[seed, it] = mssim(clean, fold(s.X, 36, 36))
+        stopped = [e is not None for _, e in s.dip_steps]
+        assert all(stopped), s.dip_steps          # early stopping fired, as in every reference run
+    mean, smean = G.mean(0), GS.mean(0)
+    lo, hi = R.min(0) - 0.01, R.max(0) + 0.01
+    assert np.all((mean >= lo) & (mean <= hi)), (mean, R.min(0), R.max(0))
+    slo, shi = RS.min(0) - 0.005, RS.max(0) + 0.005
+    assert np.all((smean >= slo) & (smean <= shi)), (smean, RS.min(0), RS.max(0))
+    # the reference's outer loop improves the cube every iteration; so must this one
+    assert np.all(np.diff(mean) > 0)
