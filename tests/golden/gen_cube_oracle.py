@@ -10,6 +10,9 @@ cube200_oracle_2iter.npz — BASELINE configs[1]: oracle.LrsPnpOracle (main_LRS_
 cube196_bb36_sc.npz — BASELINE configs[2]'s sparse coding: the oracle ISTA (fro4, Nit 100) of the
   first outer iteration over the 6,408 36x36 blocks of the 196x196x198 cube; Phi and coefficients
   of every 53rd block.
+cube512_bb36_sc.npz — BASELINE configs[3]'s sparse coding (512x512x224, 50,974 blocks): the
+  coefficients of every 53rd block and Phi of every 212th (python tests/golden/gen_cube_oracle.py
+  cube512; the oracle runs only those blocks).
 
 The oracle is itself pinned to the reference (tests/test_oracle.py, tests/golden/gen_golden.py);
 nothing here imports /root/reference.
@@ -85,8 +88,37 @@ def cube196_sc():
     np.savez_compressed(os.path.join(HERE, "cube196_bb36_sc.npz"), blocks=sel, phi=PHI[sel], coefs=X[sel])
 
 
+def cube512_sc():
+    """BASELINE configs[3]'s sparse coding (512x512x224, bb 36, 50,974 blocks, fro4, Nit 100): the
+    oracle ISTA of every 53rd block only (blocks are independent), from the first outer iteration's
+    input X = Y."""
+    Y, M, D, clean = problem(512, 512, 224, 36)
+    P, B = Y.shape
+    rows, cols = O.block_grid(P, B, 36, 36)
+    nb = rows.size
+    sel = np.arange(0, nb, BLOCK_STRIDE)
+    blocks = O.im2col(Y, 36, rows[sel], cols[sel])
+    obs = (blocks != 0).astype(np.uint8)
+    al = np.empty(sel.size, np.float32)
+    th = np.empty(sel.size, np.float64)
+    cache = {}
+    for j in range(sel.size):
+        k = obs[j].tobytes()
+        if k not in cache:
+            cache[k] = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, "fro4")
+        al[j], th[j] = cache[k]
+    t0 = time.time()
+    X, PHI = O.ista_batch(blocks, obs, D, al, th, 100)
+    print(f"cube512 sparse coding: {sel.size} of {nb} blocks ({time.time() - t0:.0f} s)", flush=True)
+    # coefficients of all selected blocks, Phi of every 4th of them (fixture size)
+    np.savez_compressed(os.path.join(HERE, "cube512_bb36_sc.npz"), blocks=sel, nb=np.int64(nb), coefs=X,
+                        phi_blocks=sel[::4], phi=PHI[::4])
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["cube196", "cube200"]
+    if "cube512" in which:
+        cube512_sc()
     if "cube196" in which:
         cube196_sc()
     if "cube200" in which:

@@ -200,6 +200,24 @@ def test_config2_sparse_coding_vs_oracle_fixture(gpu, golden):
         assert rel(ph[k], g["phi"][k]) < 1e-5, k
 
 
+def test_config3_sparse_coding_vs_oracle_fixture(gpu, golden):
+    """BASELINE configs[3]'s sparse coding at full size (512x512x224, bb 36, 50,974 blocks, fro4,
+    Nit 100; main_LRS_PnP_DIP_pro.py:375-400): the row-split ISTA kernel's coefficients of every 53rd
+    block and Phi of every 212th against the oracle C ISTA at 1e-5 relative L2."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    g = golden("cube512_bb36_sc.npz")
+    Y, M, D, _ = _bench_problem(512, 512, 224, 36)
+    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_pro(lowrank="svt"))
+    assert s.nb == int(g["nb"]) == 50974
+    phi, coefs = s.sparse_coding(want_coefs=True)
+    torch.cuda.synchronize()
+    co = coefs.index_select(0, torch.from_numpy(g["blocks"]).cuda()).cpu().numpy()
+    ph = phi.index_select(0, torch.from_numpy(g["phi_blocks"]).cuda()).cpu().numpy()[:, :1296]
+    assert rel(co, g["coefs"]) < 1e-5 and rel(ph, g["phi"]) < 1e-5
+    for k in range(co.shape[0]):
+        assert rel(co[k], g["coefs"][k]) < 1e-5, k
+
+
 @pytest.mark.parametrize("world,cube,bb", [(2, "96x64x40", 8), (3, "100x60x37", 8), (3, "100x61x37", 8),
                                            (2, "38x38x40", 36)])
 def test_row_slab_sharding_matches_whole_cube(gpu, world, cube, bb):
