@@ -1271,10 +1271,19 @@ __global__ void k_gen_phi(const float *__restrict__ R, float *__restrict__ phi, 
 
 inline unsigned gen_blocks(int64_t n) { return (unsigned)std::min<int64_t>((n + 255) / 256, 8192); }
 
+// split-K scratch for any chunk of <= kGenChunk blocks: the split count grows as the tile count falls,
+// so the need peaks at the top of each 64-row band, not at the full chunk
+int64_t ista_generic_part_floats(int64_t n, int64_t K) {
+    int64_t m = 0;
+    for (int64_t rows = 64; rows <= kGenChunk; rows += 64)
+        m = std::max(m, std::max(dense_gemm_part_floats((int)rows, (int)n, (int)K),
+                                 dense_gemm_part_floats((int)rows, (int)K, (int)n)));
+    return m;
+}
+
 size_t ista_generic_workspace(int64_t n, int64_t K) {
     const int64_t c = kGenChunk;
-    const int64_t part = std::max(dense_gemm_part_floats((int)c, (int)n, (int)K), dense_gemm_part_floats((int)c, (int)K, (int)n));
-    return (size_t)(2 * c * K + c * n + part) * sizeof(float) + 256;
+    return (size_t)(2 * c * K + c * n + ista_generic_part_floats(n, K)) * sizeof(float) + 256;
 }
 
 int ista_generic(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
@@ -1284,8 +1293,7 @@ int ista_generic(const float *Yb, const uint8_t *obs, const float *D, int64_t n,
     if (n > INT32_MAX / 2 || K > 16384) return LRS_E_UNSUPPORTED;
     const int64_t c = kGenChunk;
     float *X = (float *)ws, *G = X + c * K, *R = G + c * K, *part = R + c * n;
-    const int64_t part_cap = std::max(dense_gemm_part_floats((int)c, (int)n, (int)K),
-                                      dense_gemm_part_floats((int)c, (int)K, (int)n));
+    const int64_t part_cap = ista_generic_part_floats(n, K);
     for (int64_t j0 = 0; j0 < nb; j0 += c) {
         const int rows = (int)std::min(c, nb - j0);
         hipError_t e = hipMemsetAsync(X, 0, sizeof(float) * rows * K, st);

@@ -115,12 +115,13 @@ def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant, K):
     worst_phi = max(rel(phi[j], PHIo[j]) for j in range(nb))
     # The MATLAB variant's exp(-d/h^2) weights (no cutoff) amplify any ~1-ulp float32 difference:
     # d/h^2 ~ 1e2-1e3 at the reference's h, so the weights move by ~2 diff dg / h^2 ~ 1e-4 per
-    # iteration.  One iteration from identical inputs is held to 1e-5 (the prox itself is bit-exact,
-    # test_nlm_matlab_prox_bitexact); over several iterations the bar is the oracle's own
+    # iteration.  The fused kernels hold one iteration from identical inputs to 1e-5 (the prox itself
+    # is bit-exact, test_nlm_matlab_prox_bitexact); the generic path's GEMM rounds its gradient
+    # differently, which the weights amplify even in one iteration.  So the bar is the oracle's own
     # sensitivity: the oracle re-run on inputs perturbed by 1 float32 ulp, and the kernel may differ
     # from the oracle by at most 4x that (and 1e-5).
     tol = 1e-5
-    if variant == "matlab" and Nit > 1:
+    if variant == "matlab" and (Nit > 1 or K > 512):
         flip = np.where(rng.random(Yb.shape) < 0.5, -1.0, 1.0)
         Yp = (Yb.astype(np.float64) * (1.0 + flip * 2.0 ** -23)).astype(np.float32)
         Xp, PHIp = O.ista_batch(Yp, obs, D, alpha, thr, Nit, prox)
