@@ -260,6 +260,27 @@ def dip_flops_per_step(net):
     return tot
 
 
+def dip_alg_bytes_per_step(net):
+    """Algorithmic HBM bytes of one DIP training step: every tensor a layer must read
+    or write once, fp32.  Per conv node with input x (Cin x Pin) and output z (Cout x P): forward x
+    in, z out, BN(+act) z in, y out; backward BN gy and z in, dL/dz out, data gradient dL/dz in and
+    dL/dx out (none for a conv on the network input), weight gradient dL/dz and x in: 3 Cin Pin +
+    8 Cout P (2 Cin Pin fewer on the input, 2 Cout P fewer without BN); the loss head reads the
+    output and target and writes dL/dz (3 C P), Adam reads p, g, m, v and writes p, m, v."""
+    sh = [net.in_shape] + list(net.shapes)
+    tot = 0
+    for i, nd in enumerate(net.nodes):
+        if nd.kind != 0:
+            continue
+        ci, hi, wi = sh[nd.in0]
+        co, ho, wo = sh[i + 1]
+        xin, out = ci * hi * wi, co * ho * wo
+        tot += (xin if nd.in0 == 0 else 3 * xin) + (8 if nd.bn else 6) * out
+    co, ho, wo = sh[-1]
+    tot += 3 * co * ho * wo + 7 * net.n_params
+    return 4 * tot
+
+
 def ista_entry(name, ista_ms, flops, traffic_key, profiled=True):
     achieved = flops / (ista_ms * 1e-3) / 1e12
     return {"kernel": name, "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -316,6 +337,8 @@ def main_dip(args, ctx):
     ista_flops = nit * s.nb * 4 * n * args.K + s.nb * 2 * n * args.K
     net_desc = ("skip net (5 x 128 ch, 128-ch skips)" if pro else f"my_Lipschitz_Unet ({B}->128->{B} ch)")
     tag = "dip_pro" if pro else "dip"
+    traffic = load_traffic(f"{tag}_hbm_bytes_per_outer_iter", profiled)
+    alg_bytes = dip_alg_bytes_per_step(s.dip.net) * args.dip_steps if s.dip is not None else None
     out = {
         "metric": METRIC, "value": (1 if split else ctx.world) * args.steps / elapsed, "unit": "outer_iters/s",
         "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
@@ -337,7 +360,9 @@ def main_dip(args, ctx):
                                                 f"GEMMs, sigma_max, BN, loss, Adam kernels)",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                     "traffic": load_traffic(f"{tag}_hbm_bytes_per_outer_iter", profiled),
+                     "traffic": traffic,
+                     "alg_bytes": alg_bytes,
+                     "traffic_over_alg": (traffic / alg_bytes) if traffic and alg_bytes else None,
                      "flops_per_outer_iter": flops, "ms_per_outer_iter": dip_ms,
                      "kernels": [ista_entry(f"k_ista_rs (lrs_ista_f32: {s.nb} blocks of {n} rows, Nit {nit})",
                                             ista_ms, ista_flops, f"{tag}_ista_hbm_bytes_per_launch", profiled)]},

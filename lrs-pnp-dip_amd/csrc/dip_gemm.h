@@ -974,16 +974,18 @@ __device__ __forceinline__ void conv_prep_body(const ConvPrep &c, float s, int64
     if (c.Wn)
         for (int64_t i = i0; i < nw; i += stride) c.Wn[i] = c.W[i] / s;
     const int ed = c.upc ? 16 : (c.ke > 0 ? c.ke * c.ke : c.kk);
-    const int64_t nf = c.wf ? (int64_t)c.Cout * (c.upc ? 16 : c.kk) * c.Cp : 0, nd = c.wd ? (int64_t)c.Cin * ed * c.Cop : 0;
-    for (int64_t i = i0; i < nf + nd; i += stride) {
+    // 32-bit index arithmetic (lrs_dipnet_create and the lrs_conv2d_* entry points reject a conv whose
+    // planes reach 2^31 / 3 elements); 64-bit divisions were most of this kernel's time
+    const int nf = c.wf ? c.Cout * (c.upc ? 16 : c.kk) * c.Cp : 0, nd = c.wd ? c.Cin * ed * c.Cop : 0;
+    for (int i = (int)i0; i < nf + nd; i += (int)stride) {
         float x;
         __bf16 *dst;
-        int64_t plane, j;
+        int plane, j;
         if (c.upc) {
             int cl, e, co, ci;
             if (i < nf) {   // [cls][co][e * Cp + ci]
-                cl = (int)(i / ((int64_t)c.Cout * 4 * c.Cp));
-                const int rem = (int)(i - (int64_t)cl * c.Cout * 4 * c.Cp);
+                cl = i / (c.Cout * 4 * c.Cp);
+                const int rem = i - cl * c.Cout * 4 * c.Cp;
                 co = rem / (4 * c.Cp);
                 const int r = rem - co * 4 * c.Cp;
                 e = r / c.Cp;
@@ -991,8 +993,8 @@ __device__ __forceinline__ void conv_prep_body(const ConvPrep &c, float s, int64
                 dst = c.wf; plane = nf; j = i;
             } else {        // [ci][(4 cls + e) * Cop + co]
                 j = i - nf;
-                ci = (int)(j / (16 * c.Cop));
-                const int rem = (int)(j - (int64_t)ci * 16 * c.Cop), ce = rem / c.Cop;
+                ci = j / (16 * c.Cop);
+                const int rem = j - ci * 16 * c.Cop, ce = rem / c.Cop;
                 co = rem - ce * c.Cop;
                 cl = ce >> 2;
                 e = ce & 3;
@@ -1004,14 +1006,14 @@ __device__ __forceinline__ void conv_prep_body(const ConvPrep &c, float s, int64
                 if (c.si >= 0) x = x / s;
             }
         } else if (i < nf) {
-            const int co = (int)(i / (c.kk * c.Cp)), rem = (int)(i - (int64_t)co * c.kk * c.Cp);
+            const int co = i / (c.kk * c.Cp), rem = i - co * c.kk * c.Cp;
             const int kyx = rem / c.Cp, ci = rem - kyx * c.Cp;
             x = ci < c.Cin ? c.W[((int64_t)co * c.Cin + ci) * c.kk + kyx] : 0.0f;
             if (c.si >= 0) x = x / s;
             dst = c.wf; plane = nf; j = i;
         } else {
             j = i - nf;
-            const int ci = (int)(j / (ed * c.Cop)), rem = (int)(j - (int64_t)ci * ed * c.Cop);
+            const int ci = j / (ed * c.Cop), rem = j - ci * ed * c.Cop;
             const int e = rem / c.Cop, co = rem - e * c.Cop;
             x = 0.0f;
             if (co < c.Cout) {

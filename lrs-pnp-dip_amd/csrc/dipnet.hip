@@ -22,6 +22,7 @@ using namespace lrs;
 namespace {
 
 constexpr int kEw = 256;   // elementwise block size
+constexpr int64_t kForkBigP = 9604;   // maps from 98^2 up fork the weight-gradient stream at every conv
 
 // A/B tuning knobs.  The environment is read only by the tuning build (make TUNING=1 ->
 // liblrspnp_hip_tune.so, -DLRS_TUNING); the product library always takes the default, so a
@@ -466,11 +467,13 @@ inline int64_t implicit_min_pixels() {
 }
 
 // split w into the bf16 planes of the forward operand (and of the data-gradient one if wd)
-void wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, hipStream_t st) {
+int wprep(const ConvGeom &g, const float *w, int Cout, __bf16 *wf, __bf16 *wd, hipStream_t st) {
     const int kk = g.k * g.k;
+    if (wprep_elems(g, Cout) >= INT32_MAX / 3) return LRS_E_UNSUPPORTED;   // k_conv_prep's 32-bit indices
     const int64_t n = wprep_elems(g, Cout) / 3;
     const ConvPrep c{w, nullptr, wf, wd, Cout, g.Cin, kk, r16(g.Cin), r16(Cout), -1, g.k, wd ? up_eff_k(g) : 0};
     hipLaunchKernelGGL(k_conv_prep1, dim3(ew_blocks(n, 2048)), dim3(256), 0, st, c);
+    return LRS_OK;
 }
 
 // LRS_DIP_PW_NB = the allowed NB digits, e.g. "4" keeps 64-pixel workgroups everywhere (A/B only)
@@ -871,7 +874,7 @@ extern "C" int lrs_conv2d_fwd_f32(const float *x, int Cin, int H, int W, const f
     if (need > 0 && (!ws || ws_bytes < (size_t)need * sizeof(float))) return LRS_E_WORKSPACE;
     float *pt = implicit ? (float *)ws + cw.dcol : (float *)ws;
     __bf16 *wp = implicit ? (__bf16 *)((float *)ws + cw.dcol + cw.part) : nullptr;
-    if (implicit) wprep(g, w, Cout, wp, nullptr, (hipStream_t)stream);
+    if (implicit && (rc = wprep(g, w, Cout, wp, nullptr, (hipStream_t)stream))) return rc;
     return conv_fwd(g, x, w, bias, Cout, col, y, pt, cw.part, (hipStream_t)stream, wp);
 }
 
@@ -906,7 +909,7 @@ extern "C" int lrs_conv2d_bwd_x_f32(const float *gy, const float *x, const float
     float *dc = cw.dcol ? (float *)ws : nullptr;
     float *pt = (float *)ws + cw.dcol;
     __bf16 *wp = cw.wpre_floats ? (__bf16 *)((float *)ws + cw.dcol + cw.part) : nullptr;
-    if (wp && gx) wprep(g, w, Cout, wp, wp + wprep_fwd_elems(g, Cout), (hipStream_t)stream);
+    if (wp && gx && (rc = wprep(g, w, Cout, wp, wp + wprep_fwd_elems(g, Cout), (hipStream_t)stream))) return rc;
     return conv_bwd(g, gy, x, w, w_div, Cout, gx, gw, dc, pt, cw.part, (hipStream_t)stream, 0, true, wp);
 }
 
@@ -1065,6 +1068,8 @@ struct lrs_dipnet {
         bool sm = false;              // small map: forward / data gradient on k_conv_sm (dip_sm.h)
         bool upc = false;             // upsampled 3 x 3: forward / data gradient by output parity class
         bool sm_dgrad = false;        // ... data gradient through the adjoint table below
+        bool fork_pt = true;          // weight-gradient side stream: fork after its BN backward (else its
+                                      // weight gradient waits for the next fork point)
         int64_t adj_off = -1;         // the lists in the workspace (shorts, sm_adj_dim)
         std::vector<int> adj;         // host copy (sm_adj_table), uploaded at bind
     };
@@ -1268,12 +1273,63 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
 
 // Backward from dL/d(output) already in the last node's gradient buffer: every parameter
 // gradient into net->grads (the input gets none: the reference's DIP input needs no gradient).
+// Weight gradient of conv node i on stream ws: reads dL/dz, the layer input and the scale only.
+// scratch: its split-K partials (part2 on the side stream; part on the main one)
+int weight_grad(lrs_dipnet *net, int i, const float *x, hipStream_t ws, float *scratch) {
+    auto &N = net->nodes[i];
+    const int t = N.d.in0;
+    const float *gz = net->f(N.gz_off);
+    const float *colsrc = N.col_off >= 0 ? net->f(N.col_off) : net->tensor(t, x);
+    const bool sn = N.sn_index >= 0;
+    const float *w = sn ? net->f(N.wn_off) : net->params + N.w_off;
+    const float *wdiv = sn ? net->f(net->scale_off) + N.sn_index : nullptr;
+    if (N.sm) {   // the forward gathered inside k_conv_sm: the col for the weight gradient now
+        const int P = N.g.Ho * N.g.Wo;
+        const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min<int64_t>(N.Kc, 65535));
+        hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, ws, net->tensor(t, x), N.g, net->f(N.col_off));
+    }
+    if (N.upc)
+        return upc_wgrad(N.g, gz, net->tensor(t, x), wdiv, N.C, net->grads + N.w_off, scratch, net->part_cap, ws);
+    return conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, nullptr, net->grads + N.w_off, nullptr, scratch, net->part_cap, ws, 0,
+                    N.col_off < 0);
+}
+
+// Is conv node i a fork point of the weight-gradient side stream (Node::fork_pt, lrs_dipnet_create)?
+// LRS_DIP_FORK_SET (tuning only) = the node indices that fork instead, e.g. "13,12,11,10,7,4,1,0".
+bool fork_at(const lrs_dipnet *net, int i) {
+    static const char *set = tune_str("LRS_DIP_FORK_SET");
+    if (!set) return net->nodes[i].fork_pt;
+    for (const char *p = set; *p;) {
+        char *e = nullptr;
+        const long v = strtol(p, &e, 10);
+        if (e == p) break;
+        if (v == i) return true;
+        p = (*e == ',') ? e + 1 : e;
+    }
+    return false;
+}
+
 int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done) {
     int rc;
     const int n = (int)net->nodes.size();
     // gradient buffers: the first contribution to a tensor writes, later ones accumulate
     std::vector<char> written(n + 1, 0);
     written[n] = 1;
+    // weight gradients queued for the side stream, launched after the fork that follows node j's BN
+    // backward (every queued node's dL/dz is complete by then)
+    std::vector<int> wq;
+    int first_conv = 0;
+    while (first_conv < n && net->nodes[first_conv].d.kind != LRS_NODE_CONV) ++first_conv;
+    auto flush_w = [&](int j) -> int {
+        if (wq.empty()) return LRS_OK;
+        hipError_t e = hipEventRecord(net->ev_fork[j], st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(net->side, net->ev_fork[j], 0);
+        if (e != hipSuccess) return (int)e;
+        for (int q : wq)
+            if (const int r = weight_grad(net, q, x, net->side, net->f(net->part2_off))) return r;
+        wq.clear();
+        return LRS_OK;
+    };
     // a small-map data gradient may leave dL/dy of the next node as split-K partials, finished by
     // that node's k_reduce_bn_bwd1 (pend = the partials, pend_S their count)
     const float *pend = nullptr;
@@ -1307,26 +1363,18 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
             const float *w = sn ? net->f(N.wn_off) : net->params + N.w_off;
             float *gx = t > 0 ? net->f(net->nodes[t - 1].grad_off) : nullptr;
             const float *wdiv = sn ? net->f(net->scale_off) + N.sn_index : nullptr;
-            // weight gradient on the side stream (reads gz, the layer input and the scale only)
-            hipStream_t ws = st;
-            if (net->fork_w) {
-                hipError_t e = hipEventRecord(net->ev_fork[i], st);
-                if (e == hipSuccess) e = hipStreamWaitEvent(net->side, net->ev_fork[i], 0);
-                if (e != hipSuccess) return (int)e;
-                ws = net->side;
+            // weight gradient on the side stream (reads gz, the layer input and the scale only); the
+            // nodes between two fork points queue theirs until the next one (fork_at)
+            if (net->fork_w && !(t == 0 && i == first_conv)) {
+                wq.push_back(i);
+                if (fork_at(net, i) && (rc = flush_w(i))) return rc;
+            } else {
+                // no fork: or the first conv on the input, after which the main stream has no work left
+                // of its own (a fork there only adds the event latency to the step's tail); it uses the
+                // main stream's scratch, free by then, beside whatever the side stream still runs
+                if (net->fork_w && (rc = flush_w(i))) return rc;
+                if ((rc = weight_grad(net, i, x, st, net->f(net->part_off)))) return rc;
             }
-            if (N.sm) {   // the forward gathered inside k_conv_sm: the col for the weight gradient now
-                const int P = N.g.Ho * N.g.Wo;
-                const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min<int64_t>(N.Kc, 65535));
-                hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, ws, net->tensor(t, x), N.g, net->f(N.col_off));
-            }
-            if (N.upc)
-                rc = upc_wgrad(N.g, gz, net->tensor(t, x), wdiv, N.C, net->grads + N.w_off, net->f(net->part2_off),
-                               net->part_cap, ws);
-            else
-                rc = conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, nullptr, net->grads + N.w_off, nullptr,
-                              net->f(net->part2_off), net->part_cap, ws, 0, N.col_off < 0);
-            if (rc) return rc;
             if (gx && N.upc) {   // by output parity class over the extended source grid, then the clamp fold
                 rc = upc_dgrad(N.g, gz, (const __bf16 *)net->f(N.wpre_off) + wprep_fwd_elems(N.g, N.C, true), N.C, gx,
                                net->f(net->dcol_off), net->f(net->part_off), net->part_cap, st, written[t]);
@@ -1395,6 +1443,7 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
         }
     }
     if (net->fork_w) {   // join the side stream before anyone reads the weight gradients
+        if ((rc = flush_w(0))) return rc;
         hipError_t e = hipEventRecord(net->ev_join, net->side);
         if (e == hipSuccess) e = hipStreamWaitEvent(st, net->ev_join, 0);
         if (e != hipSuccess) return (int)e;
@@ -1459,7 +1508,8 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                 N.wn_off = ofs; ofs += align64(N.C * N.Kc);
                 if (N.C * N.Kc > net->max_w) net->max_w = N.C * N.Kc;
             }
-            if (plain_unit(N.g) && net->implicit && pw_ok(N.g, N.C) && N.P >= implicit_min_pixels()) {
+            if (plain_unit(N.g) && net->implicit && pw_ok(N.g, N.C) && N.P >= implicit_min_pixels() &&
+                wprep_elems(N.g, N.C) < INT32_MAX / 3) {
                 N.wpre_off = ofs;   // 1x1 on k_pw: its pre-split weight planes
                 ofs += align64((wprep_elems(N.g, N.C) + 1) / 2);
             }
@@ -1469,7 +1519,8 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                     // small-map conv, whose forward gathers it inside k_conv_sm)
                     N.col_off = ofs;
                     ofs += align64(N.Kc * N.P);
-                    if (net->implicit && sm_enabled() && N.d.k <= 3 && conv_implicit_ok(N.g, N.C)) {
+                    if (net->implicit && sm_enabled() && N.d.k <= 3 && conv_implicit_ok(N.g, N.C) &&
+                        wprep_elems(N.g, N.C) < INT32_MAX / 3) {
                         N.sm = true;
                         N.wpre_off = ofs;
                         ofs += align64((wprep_elems(N.g, N.C) + 1) / 2);
@@ -1484,6 +1535,8 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                     }
                 } else {
                     N.upc = upc_conv(N.g);
+                    if ((N.upc ? wprep_elems(N.g, N.C, true) : wprep_elems(N.g, N.C)) >= INT32_MAX / 3)
+                        return fail(LRS_E_UNSUPPORTED);   // k_conv_prep's 32-bit plane indices
                     N.wpre_off = ofs;
                     ofs += align64(((N.upc ? wprep_elems(N.g, N.C, true) : wprep_elems(N.g, N.C)) + 1) / 2);
                 }
@@ -1536,6 +1589,27 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
         N.out_off = ofs; ofs += align64((int64_t)N.C * N.P);
         N.grad_off = ofs; ofs += align64((int64_t)N.C * N.P);
         net->nodes.push_back(N);
+    }
+    // Fork points: every conv on a map of >= 98^2 pixels; a run of smaller maps forks every second
+    // conv in backward order (and at its end), so the side stream's cheap weight gradients of the
+    // small section go out in pairs.  Each cross-stream fork costs the critical stream time
+    // (tools/micro/event_cost.py); pairs: 196^2 step 1.317 -> 1.305 ms, triples 1.334 (A/B, the
+    // side stream then ends late).
+    {
+        int run = 0;
+        for (int i = (int)net->nodes.size() - 1; i >= 0; --i) {
+            auto &N = net->nodes[i];
+            if (N.d.kind != LRS_NODE_CONV) continue;
+            int prev = i - 1;   // the next conv in backward order
+            while (prev >= 0 && net->nodes[prev].d.kind != LRS_NODE_CONV) --prev;
+            if (N.P >= kForkBigP || prev < 0 || net->nodes[prev].P >= kForkBigP) {
+                N.fork_pt = true;
+                run = 0;
+            } else {
+                N.fork_pt = ++run == 2;
+                if (N.fork_pt) run = 0;
+            }
+        }
     }
     net->n_sn = n_sn;
     net->n_params = pofs;
