@@ -57,6 +57,11 @@ struct S3Split {
 __device__ __forceinline__ S3Split s3_split(float x) {
     S3Split r;
     r.b0 = (__bf16)x;
+#ifdef LRS_S3_CHEAPSPLIT   // timing experiment only (wrong products): the split's VALU cost
+    r.b1 = r.b0;
+    r.b2 = r.b0;
+    return r;
+#endif
     const float r1 = x - (float)r.b0;
     r.b1 = (__bf16)r1;
     r.b2 = (__bf16)(r1 - (float)r.b1);
@@ -623,21 +628,36 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
             __syncthreads();
         }
     } else {
-        if constexpr (LA::pre) la.load(m0, kbeg, kend, pa);
-        else la.load(m0, kbeg, kend, va);
-        lb.load(n0, kbeg, kend, vb);
-        for (int k0 = kbeg; k0 < kend; k0 += kS3K) {
+        // the B operand's loads two steps ahead (register sets vb / vb1, the loop unrolled by two),
+        // the A operand's one step (the weight planes hit L2; two would spill): with one wave per
+        // SIMD a single step of prefetch left the implicit-GEMM gathers exposed behind the MFMAs
+        float vb1[16];
+        auto ldA = [&](int k0) {
+            if constexpr (LA::pre) la.load(m0, k0, kend, pa);
+            else la.load(m0, k0, kend, va);
+        };
+        auto st = [&](const float (&b)[16]) {
             if constexpr (LA::pre) s3_store_pre(As, pa);
             else if constexpr (LanePix<LA>::value) wlp_store(As, va);
             else s3_store<LA::kc>(As, va);
-            if constexpr (LanePix<LB>::value) wlp_store(Bs, vb);
-            else s3_store<LB::kc>(Bs, vb);
+            if constexpr (LanePix<LB>::value) wlp_store(Bs, b);
+            else s3_store<LB::kc>(Bs, b);
+        };
+        ldA(kbeg);
+        lb.load(n0, kbeg, kend, vb);
+        if (kbeg + kS3K < kend) lb.load(n0, kbeg + kS3K, kend, vb1);
+        for (int k0 = kbeg; k0 < kend; k0 += 2 * kS3K) {
+            st(vb);
             __syncthreads();
-            if (k0 + kS3K < kend) {
-                if constexpr (LA::pre) la.load(m0, k0 + kS3K, kend, pa);
-                else la.load(m0, k0 + kS3K, kend, va);
-                lb.load(n0, k0 + kS3K, kend, vb);
-            }
+            if (k0 + kS3K < kend) ldA(k0 + kS3K);
+            if (k0 + 2 * kS3K < kend) lb.load(n0, k0 + 2 * kS3K, kend, vb);
+            mma();
+            __syncthreads();
+            if (k0 + kS3K >= kend) break;
+            st(vb1);
+            __syncthreads();
+            if (k0 + 2 * kS3K < kend) ldA(k0 + 2 * kS3K);
+            if (k0 + 3 * kS3K < kend) lb.load(n0, k0 + 3 * kS3K, kend, vb1);
             mma();
             __syncthreads();
         }
@@ -975,67 +995,59 @@ __device__ __forceinline__ void conv_prep_body(const ConvPrep &c, float s, int64
         for (int64_t i = i0; i < nw; i += stride) c.Wn[i] = c.W[i] / s;
     const int ed = c.upc ? 16 : (c.ke > 0 ? c.ke * c.ke : c.kk);
     // 32-bit index arithmetic (lrs_dipnet_create and the lrs_conv2d_* entry points reject a conv whose
-    // planes reach 2^31 / 3 elements); 64-bit divisions were most of this kernel's time
+    // planes reach 2^31 / 3 elements)
     const int nf = c.wf ? c.Cout * (c.upc ? 16 : c.kk) * c.Cp : 0, nd = c.wd ? c.Cin * ed * c.Cop : 0;
-    for (int i = (int)i0; i < nf + nd; i += (int)stride) {
-        float x;
-        __bf16 *dst;
-        int plane, j;
-        if (c.upc) {
-            int cl, e, co, ci;
-            if (i < nf) {   // [cls][co][e * Cp + ci]
-                cl = i / (c.Cout * 4 * c.Cp);
-                const int rem = i - cl * c.Cout * 4 * c.Cp;
-                co = rem / (4 * c.Cp);
-                const int r = rem - co * 4 * c.Cp;
-                e = r / c.Cp;
-                ci = r - e * c.Cp;
-                dst = c.wf; plane = nf; j = i;
-            } else {        // [ci][(4 cls + e) * Cop + co]
-                j = i - nf;
-                ci = j / (16 * c.Cop);
-                const int rem = j - ci * 16 * c.Cop, ce = rem / c.Cop;
-                co = rem - ce * c.Cop;
-                cl = ce >> 2;
-                e = ce & 3;
-                dst = c.wd; plane = nd;
-            }
-            x = 0.0f;
-            if (co < c.Cout && ci < c.Cin) {
-                x = upc_weight(c.W + ((int64_t)co * c.Cin + ci) * 9, cl >> 1, cl & 1, e >> 1, e & 1);
-                if (c.si >= 0) x = x / s;
-            }
-        } else if (i < nf) {
-            const int co = i / (c.kk * c.Cp), rem = i - co * c.kk * c.Cp;
-            const int kyx = rem / c.Cp, ci = rem - kyx * c.Cp;
-            x = ci < c.Cin ? c.W[((int64_t)co * c.Cin + ci) * c.kk + kyx] : 0.0f;
-            if (c.si >= 0) x = x / s;
-            dst = c.wf; plane = nf; j = i;
-        } else {
-            j = i - nf;
-            const int ci = j / (ed * c.Cop), rem = j - ci * ed * c.Cop;
-            const int e = rem / c.Cop, co = rem - e * c.Cop;
-            x = 0.0f;
-            if (co < c.Cout) {
-                const float *w = c.W + ((int64_t)co * c.Cin + ci) * c.kk;
-                if (c.ke > 0) {
-                    const int ey = e / c.ke, ex = e - ey * c.ke;
-                    for (int a = 0; a < 2; ++a)
-                        for (int b = 0; b < 2; ++b) {
-                            const int ky = a + c.k - 1 - ey, kx = b + c.k - 1 - ex;
-                            if (ky >= 0 && ky < c.k && kx >= 0 && kx < c.k) x = x + w[ky * c.k + kx];
-                        }
-                } else {
-                    x = w[e];
-                }
-                if (c.si >= 0) x = x / s;
-            }
-            dst = c.wd; plane = nd;
-        }
+    auto put = [&](__bf16 *dst, int plane, int j, float x) {
         const S3Split q = s3_split(x);
         dst[j] = q.b0;
         dst[plane + j] = q.b1;
         dst[2 * plane + j] = q.b2;
+    };
+    // forward planes (ci fastest: the W reads of a wave are kk floats apart)
+    for (int i = (int)i0; i < nf; i += (int)stride) {
+        float x = 0.0f;
+        if (c.upc) {   // [cls][co][e * Cp + ci]
+            const int cl = i / (c.Cout * 4 * c.Cp), rem = i - cl * c.Cout * 4 * c.Cp;
+            const int co = rem / (4 * c.Cp), r = rem - co * 4 * c.Cp, e = r / c.Cp, ci = r - e * c.Cp;
+            if (ci < c.Cin) {
+                x = upc_weight(c.W + ((int64_t)co * c.Cin + ci) * 9, cl >> 1, cl & 1, e >> 1, e & 1);
+                if (c.si >= 0) x = x / s;
+            }
+        } else {       // [co][kyx * Cp + ci]
+            const int co = i / (c.kk * c.Cp), rem = i - co * c.kk * c.Cp, kyx = rem / c.Cp, ci = rem - kyx * c.Cp;
+            if (ci < c.Cin) {
+                x = c.W[((int64_t)co * c.Cin + ci) * c.kk + kyx];
+                if (c.si >= 0) x = x / s;
+            }
+        }
+        put(c.wf, nf, i, x);
+    }
+    // data-gradient planes [ci][e * Cop + co] (W^T): a wave covers 8 ci x 8 co of one e, so its W reads
+    // touch 8 rows of W instead of 64 (co fastest alone put the lanes Cin kk floats apart)
+    const int nci8 = (c.Cin + 7) / 8, ncob = c.Cop / 8, ndt = c.wd ? nci8 * 64 * ed * ncob : 0;
+    for (int t = (int)i0; t < ndt; t += (int)stride) {
+        const int l = t & 63, r = t >> 6;
+        const int cob = r % ncob, r2 = r / ncob, e = r2 % ed, cib = r2 / ed;
+        const int ci = 8 * cib + (l >> 3), co = 8 * cob + (l & 7);
+        if (ci >= c.Cin) continue;
+        float x = 0.0f;
+        if (co < c.Cout) {
+            const float *w = c.W + ((int64_t)co * c.Cin + ci) * c.kk;
+            if (c.upc) {   // e = 4 cls + tap
+                x = upc_weight(w, (e >> 2) >> 1, (e >> 2) & 1, (e & 3) >> 1, e & 1);
+            } else if (c.ke > 0) {
+                const int ey = e / c.ke, ex = e - ey * c.ke;
+                for (int a = 0; a < 2; ++a)
+                    for (int b = 0; b < 2; ++b) {
+                        const int ky = a + c.k - 1 - ey, kx = b + c.k - 1 - ex;
+                        if (ky >= 0 && ky < c.k && kx >= 0 && kx < c.k) x = x + w[ky * c.k + kx];
+                    }
+            } else {
+                x = w[e];
+            }
+            if (c.si >= 0) x = x / s;
+        }
+        put(c.wd, nd, (ci * ed + e) * c.Cop + co, x);
     }
 }
 

@@ -1738,6 +1738,8 @@ __global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out,
     const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(P, i0 + chunk);
     double s = 0.0, sb = 0.0;
     if (vec) {
+        // one fp64 accumulator pair per float4 lane: four independent dependency chains
+        double s4[4] = {0.0, 0.0, 0.0, 0.0}, sb4[4] = {0.0, 0.0, 0.0, 0.0};
         const float4 *o4 = reinterpret_cast<const float4 *>(out + off), *t4 = reinterpret_cast<const float4 *>(target + off);
         const float4 *m4 = reinterpret_cast<const float4 *>(mask);
         float4 *g4 = reinterpret_cast<float4 *>(gz + off);
@@ -1759,13 +1761,15 @@ __global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out,
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float d = te[e] * me[e] - oe[e] * me[e];
-                    s += (double)d * (double)d;
+                    s4[e] += (double)d * (double)d;
                     ge[e] = act_bwd((-(norm * d)) * me[e], oe[e], act);
-                    sb += (double)ge[e];
+                    sb4[e] += (double)ge[e];
                 }
                 g4[h ? qb : q] = make_float4(ge[0], ge[1], ge[2], ge[3]);
             }
         }
+        s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        sb = (sb4[0] + sb4[1]) + (sb4[2] + sb4[3]);
     } else {
         for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
             const float mk = mask ? mask[i] : 1.0f;

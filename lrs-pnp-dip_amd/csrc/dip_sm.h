@@ -13,7 +13,10 @@
 //                    over the output pixels that read input pixel q through that tap (the conv's
 //                    adjoint, with reflection, stride and the x2 upsample folded into a table built
 //                    on the host, <= 2 terms per dimension): gx directly, no dcol, no col2im and no
-//                    fold.
+//                    fold;
+//   weight gradient: A = dL/dz [Cout][P] (fp32, split at the store), B = col^T gathered from x
+//                    through a per-conv tap table (SmWgrad), so no col matrix and no k_im2col
+//                    launch; without split-K (short K: the 36^2 maps) one launch finishes dW / scale.
 #pragma once
 
 #include "dip_gemm.h"
@@ -65,6 +68,7 @@ __device__ __forceinline__ void sm_frag(const SmImg &T, int row, int c, s3bf8 (&
 // A: pre-split planes, plane p of row x at P + p * pstride + x * ld (k contiguous, K and ld
 // multiples of 16); rows >= X and k >= kend read 0.  16-B buffer loads (L2-resident planes).
 struct SmPre {
+    static constexpr bool pre = true;
     const __bf16 *P;
     int64_t pstride;
     int ld, X;
@@ -172,8 +176,54 @@ struct SmAdj {
     }
 };
 
-template <class LB>
-__global__ __launch_bounds__(256, 2) void k_conv_sm(GemmArgs g, SmPre la, LB lb) {
+// A: a dense fp32 [X][ld] matrix, k contiguous (dL/dz of the weight gradient, k = output pixel);
+// split into the three planes at the LDS store
+struct SmDense {
+    static constexpr bool pre = false;
+    const float *S;
+    int ld, X;
+    __device__ __forceinline__ void load(int x0, int k0, int kend, int j, float (&v)[8]) const {
+        const int x = x0 + sm_row(j), k = k0 + 8 * sm_kg(j);
+        const float *src = S + (int64_t)x * ld + k;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = (x < X && k + u < kend) ? src[u] : 0.0f;
+    }
+};
+
+// B of the weight gradient: col^T[p][r], r = c kk + tap (dW's own column order), p = output pixel:
+// x[c] at the source pixel of (p, tap), from the conv's table tw[tap][P] of byte offsets within a
+// channel plane (kOob = zero pad; built on the host, sm_wgrad_table).  No LDS table.
+struct SmWgrad {
+    const float *X;
+    int xbytes;
+    int Kc, kk, P, plane;   // plane = Hs Ws 4 bytes
+    const int *tw;
+    __device__ __forceinline__ void setup(int, int *) {}
+    __device__ __forceinline__ void load(int x0, int k0, int kend, int j, float (&v)[8]) const {
+        const int r = x0 + sm_row(j), p0 = k0 + 8 * sm_kg(j);
+        const int c = r / kk, tap = r - c * kk;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
+        const int base = r < Kc ? c * plane : kOob;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int p = p0 + u;
+            const int o = p < kend ? tw[tap * P + p] : kOob;
+            v[u] = s3_bload(rs, o == kOob || base == kOob ? kOob : base + o, 0);
+        }
+    }
+};
+
+template <class LA>
+struct SmAReg {   // the A operand's registers for one load group
+    uint4 h[3];
+};
+template <>
+struct SmAReg<SmDense> {
+    float v[8];
+};
+
+template <class LB, class LA = SmPre>
+__global__ __launch_bounds__(256, 2) void k_conv_sm(GemmArgs g, LA la, LB lb) {
     __shared__ __attribute__((aligned(16))) SmImg As, Bs;
     __shared__ __attribute__((aligned(16))) int tab[kSmTabInts];
     const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
@@ -189,24 +239,29 @@ __global__ __launch_bounds__(256, 2) void k_conv_sm(GemmArgs g, SmPre la, LB lb)
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = s3f4{0.f, 0.f, 0.f, 0.f};
-    uint4 ha[2][3];
+    SmAReg<LA> ha[2];
     float vb[2][8];
+    auto lda = [&](int k0, int j) {
+        if constexpr (LA::pre) la.load(m0, k0, kend, j, ha[j].h);
+        else la.load(m0, k0, kend, j, ha[j].v);
+    };
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        la.load(m0, kbeg, kend, j, ha[j]);
+        lda(kbeg, j);
         lb.load(n0, kbeg, kend, j, vb[j]);
     }
     for (int k0 = kbeg; k0 < kend; k0 += kSmK) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            sm_store_pre(As, sm_row(j), sm_kg(j), ha[j]);
+            if constexpr (LA::pre) sm_store_pre(As, sm_row(j), sm_kg(j), ha[j].h);
+            else sm_store_f32(As, sm_row(j), sm_kg(j), ha[j].v);
             sm_store_f32(Bs, sm_row(j), sm_kg(j), vb[j]);
         }
         __syncthreads();
         if (k0 + kSmK < kend) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                la.load(m0, k0 + kSmK, kend, j, ha[j]);
+                lda(k0 + kSmK, j);
                 lb.load(n0, k0 + kSmK, kend, j, vb[j]);
             }
         }
@@ -238,6 +293,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_sm(GemmArgs g, SmPre la, LB lb)
                     float v = acc[a][b][r];
                     if (final_out) {
                         if (g.bias) v = v + g.bias[m];
+                        if (g.div) v = v / *g.div;
                         if (g.accum) v = C[(int64_t)m * g.N + n] + v;
                     }
                     C[(int64_t)m * g.N + n] = v;

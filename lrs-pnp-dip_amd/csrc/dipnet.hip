@@ -243,28 +243,52 @@ int64_t sm_part_floats(int M, int N, int K) {
     return s.S > 1 ? (int64_t)s.S * M * N : 0;
 }
 
-// C (+)= A B on k_conv_sm; split-K partials summed by k_gemm_reduce unless nsplit_out is given
-// (the caller then finishes the sum, e.g. k_reduce_bn1)
-template <class LB>
-int sm_launch(const SmPre &la, const LB &lb, float *C, const float *bias, int M, int N, int K, int accum, float *part,
-              int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr) {
+// C (+)= A B (+ bias) (/ *div) on k_conv_sm; split-K partials summed by k_gemm_reduce unless
+// nsplit_out is given (the caller then finishes the sum, e.g. k_reduce_bn1); one_launch: no split
+template <class LB, class LA = SmPre>
+int sm_launch(const LA &la, const LB &lb, float *C, const float *bias, int M, int N, int K, int accum, float *part,
+              int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr, const float *div = nullptr,
+              bool one_launch = false) {
     if (M <= 0 || N <= 0) return LRS_OK;
-    const Split s = sm_split(M, N, K);
+    Split s = sm_split(M, N, K);
+    if (one_launch) s = {1, (int)round_up(K, kSmK), false};
     if (nsplit_out) *nsplit_out = s.S;
-    GemmArgs g{nullptr, nullptr, C, bias, nullptr, M, N, K, s.kchunk, accum};
+    GemmArgs g{nullptr, nullptr, C, bias, div, M, N, K, s.kchunk, accum};
     if (s.S > 1) {
         if (!part || part_cap < (int64_t)s.S * M * N) return LRS_E_WORKSPACE;
         g.C = part;
     }
-    hipLaunchKernelGGL((k_conv_sm<LB>), dim3((N + 63) / 64, (M + 63) / 64, s.S), dim3(256), 0, st, g, la, lb);
+    hipLaunchKernelGGL((k_conv_sm<LB, LA>), dim3((N + 63) / 64, (M + 63) / 64, s.S), dim3(256), 0, st, g, la, lb);
     if (s.S > 1 && !nsplit_out) {
         const int64_t MN = (int64_t)M * N;
         hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, part, s.S, M, N,
-                           bias, nullptr, accum, C);
+                           bias, div, accum, C);
     }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
+
+// The weight-gradient gather table of a small-map conv: for tap t and output pixel p, the byte
+// offset within a source channel plane of the value col[(c, t)][p] reads (kOob = zero pad); [kk][P]
+std::vector<int> sm_wgrad_table(const ConvGeom &g) {
+    const int kk = g.k * g.k, P = g.Ho * g.Wo;
+    std::vector<int> t((size_t)kk * P, kOob);
+    for (int kyx = 0; kyx < kk; ++kyx)
+        for (int p = 0; p < P; ++p) {
+            const int oy = p / g.Wo, ox = p - oy * g.Wo, ky = kyx / g.k, kx = kyx - ky * g.k;
+            const int sy = conv_src(oy * g.stride + ky - g.pad, g.Hu, g.pad_mode, g.up);
+            const int sx = conv_src(ox * g.stride + kx - g.pad, g.Wu, g.pad_mode, g.up);
+            if (sy >= 0 && sx >= 0) t[(size_t)kyx * P + p] = 4 * (sy * g.Ws + sx);
+        }
+    return t;
+}
+
+// A small-map weight gradient on the side stream runs as one implicit k_conv_sm launch (no
+// k_im2col, no split-K, no reduce) up to this many output pixels; above it the explicit col +
+// split-K GEMM + reduce is faster (at 36^2: 18^2 maps 34 us one launch vs ~15 us for the three; the
+// split-K implicit form 22 vs ~20 us).  196^2 step (13^2 maps, side stream) 1.275 -> 1.263 ms; on the
+// single stream of a 36^2 net (no fork) 0.726 -> 0.735 ms, so it is used only where the net forks.
+constexpr int kSmWgradOneLaunchP = 200;
 
 // The data-gradient gather table of a small-map conv: for tap (ty, tx) and input pixel q, the
 // byte offsets (within a dL/dz plane) of the <= 2 x 2 output pixels that read q through it (the
@@ -323,6 +347,7 @@ int64_t conv_part_floats(const ConvGeom &g, int Cout) {
     m = std::max(m, s3_part_floats(g.Cin, Qp, kk * r16(Cout)));
     if (const int ke = up_eff_k(g)) m = std::max(m, s3_part_floats(g.Cin, g.Hs * g.Ws, ke * ke * r16(Cout)));
     m = std::max(m, std::max(sm_part_floats(Cout, P, kk * r16(g.Cin)), sm_part_floats(g.Cin, g.Hs * g.Ws, kk * r16(Cout))));
+    m = std::max(m, sm_part_floats(Cout, Kc, P));   // the small-map weight gradient (SmWgrad)
     return m;
 }
 
@@ -1072,6 +1097,8 @@ struct lrs_dipnet {
                                       // weight gradient waits for the next fork point)
         int64_t adj_off = -1;         // the lists in the workspace (shorts, sm_adj_dim)
         std::vector<int> adj;         // host copy (sm_adj_table), uploaded at bind
+        int64_t wtab_off = -1;        // small map: the weight gradient's gather table (sm_wgrad_table)
+        std::vector<int> wtab;
     };
     std::vector<Node> nodes;
     int C0 = 0, H = 0, W = 0;
@@ -1283,6 +1310,14 @@ int weight_grad(lrs_dipnet *net, int i, const float *x, hipStream_t ws, float *s
     const bool sn = N.sn_index >= 0;
     const float *w = sn ? net->f(N.wn_off) : net->params + N.w_off;
     const float *wdiv = sn ? net->f(net->scale_off) + N.sn_index : nullptr;
+    if (N.sm && N.wtab_off >= 0) {   // implicit col^T on k_conv_sm (SmWgrad), dW / scale in its epilogue
+        const int P = (int)N.P, kk = N.g.k * N.g.k;
+        return sm_launch(SmDense{gz, P, N.C},
+                         SmWgrad{net->tensor(t, x), N.g.Cin * N.g.Hs * N.g.Ws * 4, (int)N.Kc, kk, P,
+                                 N.g.Hs * N.g.Ws * 4, (const int *)net->f(N.wtab_off)},
+                         net->grads + N.w_off, nullptr, N.C, (int)N.Kc, P, 0, scratch, net->part_cap, ws, nullptr, wdiv,
+                         true);
+    }
     if (N.sm) {   // the forward gathered inside k_conv_sm: the col for the weight gradient now
         const int P = N.g.Ho * N.g.Wo;
         const dim3 grid((unsigned)((P + 255) / 256), (unsigned)std::min<int64_t>(N.Kc, 65535));
@@ -1524,6 +1559,11 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                         N.sm = true;
                         N.wpre_off = ofs;
                         ofs += align64((wprep_elems(N.g, N.C) + 1) / 2);
+                        if (N.P <= kSmWgradOneLaunchP && net->fork_w) {
+                            N.wtab = sm_wgrad_table(N.g);
+                            N.wtab_off = ofs;
+                            ofs += align64((int64_t)N.wtab.size());
+                        }
                         if (t0 > 0) {
                             N.adj = sm_adj_table(N.g);
                             N.sm_dgrad = !N.adj.empty();
@@ -1709,9 +1749,12 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
                                 (wd && !N.sm && !N.upc) ? up_eff_k(N.g) : 0, N.upc ? 1 : 0});
     }
     hipError_t e = hipSuccess;
-    for (const auto &N : net->nodes)
+    for (const auto &N : net->nodes) {
         if (e == hipSuccess && N.sm_dgrad)
             e = hipMemcpy(net->f(N.adj_off), N.adj.data(), sizeof(int) * N.adj.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess && N.wtab_off >= 0)
+            e = hipMemcpy(net->f(N.wtab_off), N.wtab.data(), sizeof(int) * N.wtab.size(), hipMemcpyHostToDevice);
+    }
     if (!tab.empty()) e = hipMemcpy(net->table(), tab.data(), sizeof(SnConv) * tab.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && !prep.empty())
         e = hipMemcpy(net->prep(), prep.data(), sizeof(ConvPrep) * prep.size(), hipMemcpyHostToDevice);
