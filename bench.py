@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--dip-steps", type=int, default=100, help="DIP steps per outer iteration (ES off, §8d)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--ista-slices", type=int, default=None,
+                    help="DIP workloads: launches the sparse coding's Nit is split over (LrsPnPConfig.ista_slices_dip)")
     ap.add_argument("--ista-max-wg", type=int, default=None,
                     help="workgroups of the sparse-coding kernel beside the DIP (default LrsPnPConfig's; 0 = unbounded)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -303,6 +305,8 @@ def main_dip(args, ctx):
     Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=0 if split else ctx.rank)
     dcfg = DipConfig(num_iter=args.dip_steps, early_stop=False, net="skip" if pro else "unet1lip")
     extra = {} if args.ista_max_wg is None else {"ista_max_wg_dip": args.ista_max_wg}
+    if args.ista_slices is not None:
+        extra["ista_slices_dip"] = args.ista_slices
     cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, Nit=nit, dip=dcfg, **extra)
     task = D.DipTaskSplit(Y, M, Dct, cfg, ctx, image_shape=(H, W)) if split else None
     s = task.s if split else LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
@@ -323,7 +327,10 @@ def main_dip(args, ctx):
     elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
     ops.ista = orig_ista
     mp1 = mpsnr(s.X, clean_d)
-    dip_ms, ista_ms = dip_t.mean_ms(), ista_t.mean_ms()
+    # a time-sliced sparse coding (LrsPnPConfig.ista_slices_dip) is several back-to-back launches:
+    # its time per outer iteration is their sum
+    n_sl = len(ista_t.ev) / max(1, args.steps)
+    dip_ms, ista_ms = dip_t.mean_ms(), ista_t.mean_ms() * n_sl
     if split and ctx.world > 1:   # rank 0 trained the DIP, ranks 1.. coded: take each stage from those ranks
         per = D.gather_scalars([dip_ms, ista_ms], ctx)
         if per is not None:
@@ -364,7 +371,8 @@ def main_dip(args, ctx):
                      "alg_bytes": alg_bytes,
                      "traffic_over_alg": (traffic / alg_bytes) if traffic and alg_bytes else None,
                      "flops_per_outer_iter": flops, "ms_per_outer_iter": dip_ms,
-                     "kernels": [ista_entry(f"k_ista_rs (lrs_ista_f32: {s.nb} blocks of {n} rows, Nit {nit})",
+                     "kernels": [ista_entry(f"k_ista_rs (lrs_ista_f32: {s.nb} blocks of {n} rows, Nit {nit}"
+                                            + (f" over {n_sl:.0f} warm-started launches" if n_sl > 1 else "") + ")",
                                             ista_ms, ista_flops, f"{tag}_ista_hbm_bytes_per_launch", profiled)]},
         "mpsnr": {"input": mp0, "after_steps": mp1, "outer_iterations_run": args.warmup + args.steps},
     }

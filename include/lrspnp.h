@@ -116,7 +116,12 @@ typedef struct {
     int32_t algorithm;    /* LRS_ISTA_ALGO_AUTO: the fused kernels for K <= 512, the generic path above;
                              LRS_ISTA_ALGO_GENERIC: every inner iteration as two dense fp32-accurate
                              GEMMs + the prox kernel, chunks of 4096 blocks (any K <= 16384) */
-    int32_t reserved[5];
+    int32_t warm_start;   /* 1: start from x0 = coefs (on input) instead of 0 and write the result back to
+                             coefs, so Nit iterations split over several calls give exactly the
+                             iterates of one call (the time-sliced sparse coding beside the DIP, see
+                             DESIGN.md §5).  Row-split kernel only (n_pad > 64 or K != 256):
+                             LRS_E_UNSUPPORTED elsewhere or without coefs. */
+    int32_t reserved[4];
 } lrs_ista_opts;
 size_t lrs_ista_workspace(int64_t n, int64_t K, int prox, const lrs_ista_opts *opts);
 int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad,

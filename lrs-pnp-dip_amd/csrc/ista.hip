@@ -1213,7 +1213,7 @@ namespace lrs {
 size_t ista_rs_workspace(int64_t n, int64_t K);
 int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
                    const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi, void *ws,
-                   size_t ws_bytes, int64_t max_wg, hipStream_t st);
+                   size_t ws_bytes, int64_t max_wg, hipStream_t st, const float *x0);
 int nlm_matlab_col_launch(const float *g, int64_t ldg, float *out, int64_t ldo, int64_t K, int64_t nvec, double h,
                           const double *h_per_vec, hipStream_t st);
 int64_t dense_gemm_part_floats(int M, int N, int K);
@@ -1361,6 +1361,7 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     const int64_t max_wg = opts ? opts->max_workgroups : 0;
     if (max_wg < 0) return LRS_E_INVALID;
     if (opts && opts->algorithm != LRS_ISTA_ALGO_AUTO && opts->algorithm != LRS_ISTA_ALGO_GENERIC) return LRS_E_INVALID;
+    if (opts && opts->warm_start != 0 && opts->warm_start != 1) return LRS_E_INVALID;
     if (n_pad % 16 != 0 || n_pad < n) return LRS_E_INVALID;
     if (prox != LRS_PROX_NLM && prox != LRS_PROX_SOFT && prox != LRS_PROX_NLM_MATLAB) return LRS_E_INVALID;
     if (n_pad > (int64_t)1 << 20 || nb > ((int64_t)1 << 40)) return LRS_E_INVALID;
@@ -1368,8 +1369,11 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     hipStream_t st = (hipStream_t)stream;
     if (ista_use_generic(K, opts))
         return ista_generic(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, st);
+    const bool warm = opts && opts->warm_start;
+    if (warm && (!coefs || ista_use_generic(K, opts) || ista_resident(n_pad, K, prox))) return LRS_E_UNSUPPORTED;
     if (!ista_resident(n_pad, K, prox))
-        return ista_rs_launch(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, max_wg, st);
+        return ista_rs_launch(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, max_wg, st,
+                              warm ? coefs : nullptr);
     IstaParams p{Yb, obs, D, alpha, thr, coefs, phi, (int)n, (int)n_pad, Nit, prox, nb, 7.0};
     const int64_t blocks_per_wg = (int64_t)kIstaWaves * 16;
     dim3 grid((unsigned)((nb + blocks_per_wg - 1) / blocks_per_wg));

@@ -45,6 +45,7 @@ struct IstaRsParams {
     int n_pad, K, Nit, prox;
     int64_t nb;
     double seven;
+    const float *x0;       // [nb][K] start coefficients (lrs_ista_opts.warm_start; may alias coefs) or null = 0
 };
 
 // numpy 'reflect' (no edge repeat) of index i into [0, K)
@@ -167,7 +168,18 @@ __global__ __launch_bounds__(256, MINW) void k_ista_rs(IstaRsParams p) {
     double krow[7];
     nlm_matlab_krow_d(krow);
 
-    for (int i = threadIdx.x; i < NQ * 64; i += 64 * S) xbuf[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // x0 = 0, or the coefficients a previous launch left (warm start: the iteration continues exactly;
+    // each workgroup reads and later writes only its own blocks' rows, so x0 may alias coefs)
+    for (int i = threadIdx.x; i < NQ * 64; i += 64 * S) {
+        floatx4 v = {0.f, 0.f, 0.f, 0.f};
+        const int64_t jb = tile * 16 + (i & 15);
+        const int a0 = 16 * (i >> 6) + 4 * ((i & 63) >> 4);
+        if (p.x0 && jb < p.nb)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (a0 + e < K) v[e] = p.x0[jb * K + a0 + e];
+        xbuf[i] = v;
+    }
 
     // fragment k of row tile t: k < NQ -> DAf q = k, else DTf q = k - NQ.  Buffer loads: the lane's
     // 16-byte offset is the only VGPR, the wave-uniform fragment offset goes in soffset.
@@ -480,7 +492,7 @@ static int launch_rs(const IstaRsParams &p, int NT, int64_t max_wg, hipStream_t 
 
 int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
                    const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi, void *ws,
-                   size_t ws_bytes, int64_t max_wg, hipStream_t st) {
+                   size_t ws_bytes, int64_t max_wg, hipStream_t st, const float *x0) {
     if (K < 1 || K > 512) return LRS_E_UNSUPPORTED;
     const int NQ = rs_nq(K);
     const int NT = (int)(n_pad / 16);
@@ -495,7 +507,7 @@ int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t 
         hipLaunchKernelGGL(k_ista_rs_prep, dim3(blocks), dim3(256), 0, st, D, (int)n, (int)K, NT, NQ, DAf, DTf);
         LRS_CHECK_LAUNCH();
     }
-    IstaRsParams p{Yb, obs, DAf, DTf, alpha, thr, coefs, phi, (int)n_pad, (int)K, Nit, prox, nb, 7.0};
+    IstaRsParams p{Yb, obs, DAf, DTf, alpha, thr, coefs, phi, (int)n_pad, (int)K, Nit, prox, nb, 7.0, x0};
     switch (NQ) {
     case 4: return launch_rs<4, 2>(p, NT, max_wg, st);
     case 8: return launch_rs<8, 2>(p, NT, max_wg, st);

@@ -34,15 +34,16 @@ ISTA_ALGO_AUTO, ISTA_ALGO_GENERIC = 0, 1
 
 class IstaOpts(ctypes.Structure):
     _fields_ = [("precision", ctypes.c_int32), ("max_workgroups", ctypes.c_int32), ("algorithm", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 5)]
+                ("warm_start", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
 class DipOpts(ctypes.Structure):
     _fields_ = [("precision", ctypes.c_int32), ("upsample_dgrad", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
 
 
-def ista_opts(precision: int = ISTA_SPLIT_BF16, max_workgroups: int = 0, algorithm: int = ISTA_ALGO_AUTO) -> IstaOpts:
-    return IstaOpts(precision=precision, max_workgroups=max_workgroups, algorithm=algorithm)
+def ista_opts(precision: int = ISTA_SPLIT_BF16, max_workgroups: int = 0, algorithm: int = ISTA_ALGO_AUTO,
+              warm_start: int = 0) -> IstaOpts:
+    return IstaOpts(precision=precision, max_workgroups=max_workgroups, algorithm=algorithm, warm_start=warm_start)
 
 
 def dip_opts(precision: int = DIP_SPLIT_BF16, upsample_dgrad: int = 0) -> DipOpts:

@@ -129,11 +129,12 @@ def ista_workspace(n: int, K: int, prox: int, device, algorithm: int = 0) -> tor
 
 def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=None, coefs=None,
          want_coefs=False, ws=None, stream=None, precision: int | None = None, max_workgroups: int = 0,
-         algorithm: int = 0):
+         algorithm: int = 0, warm_start: bool = False):
     """Masked ISTA + prox over all blocks; returns phi (nb, n_pad) [, coefs (nb, K)].  `ws`: an
     ista_workspace() buffer (allocated here when None and needed).  precision / max_workgroups /
-    algorithm: this call's lrs_ista_opts (None / 0 = the library defaults; algorithm 1 = the generic
-    dense-GEMM path that K > 512 always takes)."""
+    algorithm / warm_start: this call's lrs_ista_opts (None / 0 = the library defaults; algorithm 1 =
+    the generic dense-GEMM path that K > 512 always takes; warm_start: continue from `coefs`, which
+    must be given, and write the result back to it)."""
     L = device_lib()
     _dev(Yb, torch.float32, "Yb")
     _dev(obs, torch.uint8, "obs")
@@ -144,14 +145,18 @@ def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=Non
     K = D.shape[1]
     if phi is None:
         phi = torch.empty((nb, n_pad), dtype=torch.float32, device=Yb.device)
+    if warm_start:
+        if coefs is None:
+            raise LrsError("ista(warm_start=True) continues from `coefs`: pass it")
+        want_coefs = True
     if want_coefs and coefs is None:
         coefs = torch.empty((nb, K), dtype=torch.float32, device=Yb.device)
     if ws is None:
         ws = ista_workspace(n, K, prox, Yb.device, algorithm)
     opts = None
-    if precision is not None or max_workgroups or algorithm:
+    if precision is not None or max_workgroups or algorithm or warm_start:
         opts = ctypes.byref(_libmod.ista_opts(_libmod.ISTA_SPLIT_BF16 if precision is None else int(precision),
-                                              int(max_workgroups), int(algorithm)))
+                                              int(max_workgroups), int(algorithm), 1 if warm_start else 0))
     check(L.lrs_ista_f32(_p(Yb), _p(obs), _p(D), n, n_pad, K, nb, _p(alpha), _p(thr), int(Nit), int(prox),
                          _p(coefs) if want_coefs else None, _p(phi), opts, _p(ws), 0 if ws is None else ws.numel(),
                          _s(stream)), "lrs_ista_f32")

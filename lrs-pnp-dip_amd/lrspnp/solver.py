@@ -42,6 +42,13 @@ class LrsPnPConfig:
     # (bench.py --ista-max-wg): 0 -> 7.25 outer it/s, 128 -> 7.18, 64 -> 6.97, 32 -> 6.68: a longer,
     # narrower sparse coding taxes the DIP more than a short full-chip one, so unbounded.
     ista_max_wg_dip: int = 0
+    # Launches the sparse coding's Nit iterations are split over beside the DIP training
+    # (lowrank='dip'; lrs_ista_opts.warm_start: the iterates are exactly those of one launch).  A
+    # workgroup of one launch holds its CU for the whole Nit; slices free CUs for the DIP's kernels
+    # every Nit / slices iterations.  Measured at configs[2] (bench.py --ista-slices, 2 rounds):
+    # 1 -> 7.50 outer it/s, 4 -> 7.49, 10 -> 7.39-7.42, 25 -> 7.27 (each slice re-forms D^T(m.*y) and
+    # Phi, and runs longer beside the DIP than its share of one launch), so one launch.
+    ista_slices_dip: int = 1
 
     @staticmethod
     def dip_1lip(**kw) -> "LrsPnPConfig":
@@ -250,8 +257,21 @@ class LrsPnP:
         # sparse coding is enqueued first so it runs beside the DIP training
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
                    stream=main)
-        ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
-                 ws=self.ista_ws, stream=main, max_workgroups=self.cfg.ista_max_wg_dip)
+        rs = self.n_pad > 64 and self.D.shape[1] <= 512   # the row-split kernel (warm start) serves
+        sl = max(1, min(int(self.cfg.ista_slices_dip), self.cfg.Nit)) if rs else 1
+        if sl == 1:
+            ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
+                     ws=self.ista_ws, stream=main, max_workgroups=self.cfg.ista_max_wg_dip)
+        else:   # time-sliced: Nit split over `sl` launches continuing from the coefficients
+            if getattr(self, "_coefs", None) is None:
+                self._coefs = torch.empty((self.nb, self.D.shape[1]), dtype=torch.float32, device=self.Yb.device)
+            done = 0
+            for k in range(sl):
+                it = (self.cfg.Nit * (k + 1)) // sl - done
+                ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, it, self.prox, phi=self.phi,
+                         coefs=self._coefs, want_coefs=True, warm_start=k > 0, ws=self.ista_ws, stream=main,
+                         max_workgroups=self.cfg.ista_max_wg_dip)
+                done += it
         self.low_rank_dip(lr)
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,

@@ -185,6 +185,36 @@ def test_ista_bounded_grid_is_bitwise_the_same(ops):
     assert max(rel(out[0][1][j], Xo[j]) for j in range(nb)) < 1e-5
 
 
+@pytest.mark.parametrize("K,prox", [(256, "nlm"), (100, "nlm"), (512, "soft"), (256, "matlab")])
+def test_ista_warm_start_slices_are_one_launch(ops, K, prox):
+    """lrs_ista_opts.warm_start (the time-sliced sparse coding beside the DIP, LrsPnPConfig.
+    ista_slices_dip): Nit iterations split over several launches that continue from the coefficients
+    give the one-launch Phi and coefficients bit for bit; unsupported (no coefs) is refused."""
+    from lrspnp.data import synthetic_dictionary
+    from lrspnp._lib import LrsError
+    rng = np.random.default_rng(5)
+    n, nb = 36 * 36, 16 * 3 + 7
+    pr = {"nlm": ops.PROX_NLM, "soft": ops.PROX_SOFT, "matlab": ops.PROX_NLM_MATLAB}[prox]
+    D = synthetic_dictionary(n, K, seed=4)
+    Yb, obs = _rand_blocks(rng, nb, n, 0.2)
+    alpha = np.empty(nb, np.float32); thr = np.empty(nb, np.float64)
+    for j in range(nb):
+        alpha[j], thr[j] = O.ista_alpha_h(D[obs[j].astype(bool)], 0.1, "soft" if prox == "soft" else "fro4")
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    args = (d(Yb), d(obs), d(D), n, d(alpha), d(thr))
+    phi1, co1 = ops.ista(*args, 13, pr, want_coefs=True)
+    co = torch.full((nb, K), float("nan"), device="cuda")
+    done = 0
+    for k, it in enumerate((4, 1, 5, 3)):
+        phi, _ = ops.ista(*args, it, pr, coefs=co, want_coefs=True, warm_start=k > 0)
+        done += it
+    torch.cuda.synchronize()
+    assert done == 13
+    assert torch.equal(phi, phi1) and torch.equal(co, co1)
+    with pytest.raises(LrsError):
+        ops.ista(*args, 2, pr, warm_start=True)
+
+
 def test_ista_kernel_vs_reference_golden(ops, golden):
     """Reference `ista` outputs (captured from the unmodified reference, gen_golden.py)."""
     from lrspnp.data import synthetic_dictionary
