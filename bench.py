@@ -52,7 +52,7 @@ import numpy as np  # noqa: E402
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table (f32 MFMA = f32 vector peak)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02", "traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03", "traffic.json")
 
 
 def parse():
@@ -112,7 +112,7 @@ def make_problem(H, W, B, bb, K, seed):
 
 
 def load_traffic(key, profiled=True):
-    """HBM bytes of the committed PMC pass (profiles/r02/traffic.json); None for a configuration
+    """HBM bytes of the committed PMC pass (profiles/r03/traffic.json); None for a configuration
     other than the profiled default one."""
     if not profiled:
         return None
