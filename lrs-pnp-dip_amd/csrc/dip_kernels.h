@@ -1826,6 +1826,19 @@ __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float
                        float *__restrict__ v, int64_t n, const int *step, float lr, float b1, float b2,
                        float eps) {
     __shared__ float sc[2];   // the bias corrections, once per workgroup (fp64 pow is costly)
+    const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
+    const int64_t n4 = vec ? n / 4 : 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the first float4 of every thread is loaded before thread 0's fp64 pow: the loads' latency and
+    // the bias corrections overlap (one float4 per thread covers the whole net at the launch size)
+    float4 pv0 = {0.f, 0.f, 0.f, 0.f}, mv0 = pv0, vv0 = pv0, gv0 = pv0;
+    if (q0 < n4) {
+        pv0 = reinterpret_cast<float4 *>(p)[q0];
+        mv0 = reinterpret_cast<float4 *>(m)[q0];
+        vv0 = reinterpret_cast<float4 *>(v)[q0];
+        gv0 = reinterpret_cast<const float4 *>(g)[q0];
+    }
     if (threadIdx.x == 0) {
         const int t = *step;
         const double bc1 = 1.0 - pow((double)b1, (double)t);
@@ -1842,13 +1855,11 @@ __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float
         const float den = sqrtf(vi) / bc2s + eps;
         pi = pi - step_size * (mi / den);
     };
-    const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
-    const int64_t n4 = vec ? n / 4 : 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
-        float4 pv = reinterpret_cast<float4 *>(p)[q], mv = reinterpret_cast<float4 *>(m)[q],
-               vv = reinterpret_cast<float4 *>(v)[q];
-        const float4 gv = reinterpret_cast<const float4 *>(g)[q];
+    for (int64_t q = q0; q < n4; q += stride) {
+        const bool first = q == q0;
+        float4 pv = first ? pv0 : reinterpret_cast<float4 *>(p)[q], mv = first ? mv0 : reinterpret_cast<float4 *>(m)[q],
+               vv = first ? vv0 : reinterpret_cast<float4 *>(v)[q];
+        const float4 gv = first ? gv0 : reinterpret_cast<const float4 *>(g)[q];
         upd(pv.x, gv.x, mv.x, vv.x);
         upd(pv.y, gv.y, mv.y, vv.y);
         upd(pv.z, gv.z, mv.z, vv.z);
