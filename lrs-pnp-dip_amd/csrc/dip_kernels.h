@@ -1822,9 +1822,34 @@ __global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out,
 // Adam (torch.optim.Adam defaults: no weight decay, no amsgrad), flat parameter buffer.
 // step is a device counter so a captured step replays correctly.
 // ------------------------------------------------------------------------------------------
+// A weight gradient whose split-K partials Adam itself finishes (the step's last weight gradient,
+// lrs_dipnet_train_steps): parameters [beg, beg + len) take g = (sum of the nsplit partials, in
+// k_gemm_reduce's order) / *div, which is also stored to the gradient buffer
+struct AdamPend {
+    const float *part;
+    int nsplit;
+    int64_t beg, len;
+    const float *div;
+    float *gout;
+};
+
+__device__ __forceinline__ float adam_pend_grad(const AdamPend &a, int64_t idx) {
+    const int64_t i = idx - a.beg;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 8 <= a.nsplit; z += 8)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] += a.part[(int64_t)(z + u) * a.len + i];
+    for (; z < a.nsplit; ++z) acc[z & 7] += a.part[(int64_t)z * a.len + i];
+    float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    if (a.div) s = s / *a.div;
+    a.gout[idx] = s;
+    return s;
+}
+
 __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
                        float *__restrict__ v, int64_t n, const int *step, float lr, float b1, float b2,
-                       float eps) {
+                       float eps, AdamPend pend) {
     __shared__ float sc[2];   // the bias corrections, once per workgroup (fp64 pow is costly)
     const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
     const int64_t n4 = vec ? n / 4 : 0;
@@ -1859,7 +1884,19 @@ __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float
         const bool first = q == q0;
         float4 pv = first ? pv0 : reinterpret_cast<float4 *>(p)[q], mv = first ? mv0 : reinterpret_cast<float4 *>(m)[q],
                vv = first ? vv0 : reinterpret_cast<float4 *>(v)[q];
-        const float4 gv = first ? gv0 : reinterpret_cast<const float4 *>(g)[q];
+        float4 gv = first ? gv0 : reinterpret_cast<const float4 *>(g)[q];
+        if (pend.part && 4 * q + 3 >= pend.beg && 4 * q < pend.beg + pend.len) {
+            if (4 * q >= pend.beg && 4 * q + 3 < pend.beg + pend.len) {
+                gv.x = adam_pend_grad(pend, 4 * q); gv.y = adam_pend_grad(pend, 4 * q + 1);
+                gv.z = adam_pend_grad(pend, 4 * q + 2); gv.w = adam_pend_grad(pend, 4 * q + 3);
+            } else {
+                float ge[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (4 * q + e >= pend.beg && 4 * q + e < pend.beg + pend.len) ge[e] = adam_pend_grad(pend, 4 * q + e);
+                gv = make_float4(ge[0], ge[1], ge[2], ge[3]);
+            }
+        }
         upd(pv.x, gv.x, mv.x, vv.x);
         upd(pv.y, gv.y, mv.y, vv.y);
         upd(pv.z, gv.z, mv.z, vv.z);
@@ -1870,7 +1907,8 @@ __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float
     }
     for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         float pi = p[i], mi = m[i], vi = v[i];
-        upd(pi, g[i], mi, vi);
+        const float gi = (pend.part && i >= pend.beg && i < pend.beg + pend.len) ? adam_pend_grad(pend, i) : g[i];
+        upd(pi, gi, mi, vi);
         m[i] = mi;
         v[i] = vi;
         p[i] = pi;

@@ -597,7 +597,7 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
 // weight planes (wprep) for the stride-1 data gradient.
 int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *w, const float *div, int Cout,
              float *gx, float *gw, float *dcol, float *part, int64_t part_cap, hipStream_t st, int accum_gx = 0,
-             bool implicit = false, const __bf16 *wpre = nullptr) {
+             bool implicit = false, const __bf16 *wpre = nullptr, int *wsplit_out = nullptr) {
     const int P = g.Ho * g.Wo, kk = g.k * g.k, Kc = g.Cin * kk;
     int rc;
     implicit = implicit && !plain_unit(g);
@@ -606,8 +606,9 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         // data gradient only (the weight gradient runs elsewhere)
     } else if (implicit) {
         if (!conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
+        // wsplit_out: the caller finishes the split-K sum (k_adam's AdamPend)
         rc = gemm_s3_conv(LdDense<true>{gz, P, Cout}, LdWgradTM{col, g.Cin * g.Hs * g.Ws * 4, g, nullptr, 0}, gw,
-                          nullptr, div, Cout, Kc, P, part, part_cap, st);
+                          nullptr, div, Cout, Kc, P, part, part_cap, st, wsplit_out);
     } else {
         // a 1x1 conv's weight gradient (K = all pixels): 128-tiles with deep split-K on the split-bf16
         // kernel (A/B in the 196^2 training step, configs[2]: 5.50 -> 5.65 outer it/s against the f32
@@ -1025,7 +1026,7 @@ extern "C" int lrs_adam_f32(float *p, const float *g, float *m, float *v, int64_
     if (!p || !g || !m || !v || !step || n < 0) return LRS_E_INVALID;
     if (n == 0) return LRS_OK;
     hipLaunchKernelGGL(k_adam, dim3(ew_blocks((n + 3) / 4, 8192)), dim3(kEw), 0, (hipStream_t)stream, p, g, m, v, n, step, lr,
-                       beta1, beta2, eps);
+                       beta1, beta2, eps, AdamPend{});
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -1246,7 +1247,7 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
     return LRS_OK;
 }
 
-int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done = false);
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done = false, AdamPend *pw = nullptr);
 int mse_head(lrs_dipnet *net, const float *out, const float *target, const float *mask, hipStream_t st);
 
 // k_mse_head over the last node (conv without BN): gz and the bias gradient of that node, + loss
@@ -1286,10 +1287,14 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
         rc = lrs_masked_mse_f32(out, target, mask, Lst.C, Lst.P, net->f(Lst.grad_off), net->loss_acc(), st);
     }
     if (rc) return rc;
-    rc = dipnet_backward(net, x, st, net->head_fusable);
+    // the input conv's weight-gradient split-K sum is finished inside Adam (one launch less on the
+    // step's tail)
+    AdamPend pw{};
+    rc = dipnet_backward(net, x, st, net->head_fusable, &pw);
     if (rc) return rc;
-    rc = lrs_adam_f32(net->params, net->grads, net->am, net->av, net->n_params, net->step(), lr, b1, b2, eps, st);
-    if (rc) return rc;
+    hipLaunchKernelGGL(k_adam, dim3(ew_blocks((net->n_params + 3) / 4, 8192)), dim3(kEw), 0, st, net->params,
+                       (const float *)net->grads, net->am, net->av, net->n_params, (const int *)net->step(), lr, b1, b2,
+                       eps, pw);
     if (es) {
         rc = es_update(out, (int64_t)Lst.C * Lst.P, ring, es, st);
         if (rc) return rc;
@@ -1302,7 +1307,8 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
 // gradient into net->grads (the input gets none: the reference's DIP input needs no gradient).
 // Weight gradient of conv node i on stream ws: reads dL/dz, the layer input and the scale only.
 // scratch: its split-K partials (part2 on the side stream; part on the main one)
-int weight_grad(lrs_dipnet *net, int i, const float *x, hipStream_t ws, float *scratch) {
+int weight_grad(lrs_dipnet *net, int i, const float *x, hipStream_t ws, float *scratch, int *wsplit_out = nullptr) {
+    if (wsplit_out) *wsplit_out = 1;
     auto &N = net->nodes[i];
     const int t = N.d.in0;
     const float *gz = net->f(N.gz_off);
@@ -1326,7 +1332,7 @@ int weight_grad(lrs_dipnet *net, int i, const float *x, hipStream_t ws, float *s
     if (N.upc)
         return upc_wgrad(N.g, gz, net->tensor(t, x), wdiv, N.C, net->grads + N.w_off, scratch, net->part_cap, ws);
     return conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, nullptr, net->grads + N.w_off, nullptr, scratch, net->part_cap, ws, 0,
-                    N.col_off < 0);
+                    N.col_off < 0, nullptr, wsplit_out);
 }
 
 // Is conv node i a fork point of the weight-gradient side stream (Node::fork_pt, lrs_dipnet_create)?
@@ -1344,7 +1350,9 @@ bool fork_at(const lrs_dipnet *net, int i) {
     return false;
 }
 
-int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done) {
+// pw (lrs_dipnet_train_steps): the input conv's weight gradient may leave its split-K partials for
+// k_adam to finish (AdamPend; pw->part == nullptr when nothing is pending)
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done, AdamPend *pw) {
     int rc;
     const int n = (int)net->nodes.size();
     // gradient buffers: the first contribution to a tensor writes, later ones accumulate
@@ -1408,7 +1416,13 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
                 // of its own (a fork there only adds the event latency to the step's tail); it uses the
                 // main stream's scratch, free by then, beside whatever the side stream still runs
                 if (net->fork_w && (rc = flush_w(i))) return rc;
-                if ((rc = weight_grad(net, i, x, st, net->f(net->part_off)))) return rc;
+                int wsplit = 1;
+                const bool defer = pw && t == 0 && i == first_conv;
+                if ((rc = weight_grad(net, i, x, st, net->f(net->part_off), defer ? &wsplit : nullptr))) return rc;
+                if (defer && wsplit > 1)
+                    *pw = AdamPend{net->f(net->part_off), wsplit, N.w_off, (int64_t)N.C * N.Kc,
+                                   N.sn_index >= 0 ? net->f(net->scale_off) + N.sn_index : nullptr,
+                                   net->grads};
             }
             if (gx && N.upc) {   // by output parity class over the extended source grid, then the clamp fold
                 rc = upc_dgrad(N.g, gz, (const __bf16 *)net->f(N.wpre_off) + wprep_fwd_elems(N.g, N.C, true), N.C, gx,
