@@ -71,6 +71,8 @@ def parse():
                     help="DIP workloads: launches the sparse coding's Nit is split over (LrsPnPConfig.ista_slices_dip)")
     ap.add_argument("--ista-max-wg", type=int, default=None,
                     help="workgroups of the sparse-coding kernel beside the DIP (default LrsPnPConfig's; 0 = unbounded)")
+    ap.add_argument("--lowrank-priority", type=int, default=None,
+                    help="priority of the low-rank (DIP) stream (LrsPnPConfig.lowrank_priority; negative = higher)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group: nccl (= RCCL, one GPU per rank) or gloo (rehearsal: rank r on GPU "
@@ -307,6 +309,8 @@ def main_dip(args, ctx):
     extra = {} if args.ista_max_wg is None else {"ista_max_wg_dip": args.ista_max_wg}
     if args.ista_slices is not None:
         extra["ista_slices_dip"] = args.ista_slices
+    if args.lowrank_priority is not None:
+        extra["lowrank_priority"] = args.lowrank_priority
     cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, Nit=nit, dip=dcfg, **extra)
     task = D.DipTaskSplit(Y, M, Dct, cfg, ctx, image_shape=(H, W)) if split else None
     s = task.s if split else LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))

@@ -1823,11 +1823,11 @@ extern "C" int lrs_dipnet_forward(lrs_dipnet *net, const float *x, void *stream)
     return dipnet_forward(net, x, (hipStream_t)stream);
 }
 
-static int ensure_side(lrs_dipnet *net);
+static int ensure_side(lrs_dipnet *net, hipStream_t st);
 
 extern "C" int lrs_dipnet_backward(lrs_dipnet *net, const float *x, const float *gout, void *stream) {
     if (!net || !net->ws || !x || !gout) return LRS_E_INVALID;
-    if (const int rs = ensure_side(net)) return rs;
+    if (const int rs = ensure_side(net, (hipStream_t)stream)) return rs;
     hipStream_t st = (hipStream_t)stream;
     const auto &Lst = net->nodes.back();
     const hipError_t e = hipMemcpyAsync(net->f(Lst.grad_off), gout, sizeof(float) * Lst.C * Lst.P,
@@ -1864,9 +1864,14 @@ extern "C" const float *lrs_dipnet_node_buffer(const lrs_dipnet *net, int node, 
 
 // The side stream and its fork/join events are created on the first training call (outside any
 // capture), so that creating a net and querying its layout needs no device.
-static int ensure_side(lrs_dipnet *net) {
+// The side stream takes the priority of the stream of that first call, so a caller that trains the
+// net on a high-priority stream (LrsPnPConfig.lowrank_priority) gets its weight gradients placed
+// with the same priority.
+static int ensure_side(lrs_dipnet *net, hipStream_t st) {
     if (!net->fork_w || net->side) return LRS_OK;
-    hipError_t e = hipStreamCreateWithFlags(&net->side, hipStreamNonBlocking);
+    int prio = 0;
+    hipError_t e = hipStreamGetPriority(st, &prio);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&net->side, hipStreamNonBlocking, prio);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming);
     for (size_t i = 0; i < net->ev_fork.size() && e == hipSuccess; ++i)
         e = hipEventCreateWithFlags(&net->ev_fork[i], hipEventDisableTiming);
@@ -1878,7 +1883,7 @@ extern "C" int lrs_dipnet_train_steps(lrs_dipnet *net, const float *x, const flo
                                       int nsteps, int use_graph, void *stream) {
     if (!net || !net->ws || !x || !target || nsteps < 0 || (es && !ring)) return LRS_E_INVALID;
     hipStream_t st = (hipStream_t)stream;
-    if (const int rs = ensure_side(net)) return rs;
+    if (const int rs = ensure_side(net, (hipStream_t)stream)) return rs;
     if (!use_graph) {
         for (int s = 0; s < nsteps; ++s) {
             const int rc = dipnet_step(net, x, target, mask, lr, beta1, beta2, eps, es, ring, st);

@@ -142,10 +142,12 @@ class DipNet:
     """A sequential conv net on the HIP engine (lrs_dipnet_*), with flat parameter buffers."""
 
     def __init__(self, nodes: list[DipNode], C: int, H: int, W: int, device="cuda", params=None, bnstats=None,
-                 precision: int = _lib.DIP_SPLIT_BF16, upsample_dgrad: int = 0):
+                 precision: int = _lib.DIP_SPLIT_BF16, upsample_dgrad: int = 0, stream_priority: int = 0):
         """params / bnstats (optional): existing flat device buffers to bind (shared with another
         engine of the same nodes at another H x W: the parameter layout does not depend on it).
-        precision / upsample_dgrad: this net's lrs_dip_opts, fixed at creation."""
+        precision / upsample_dgrad: this net's lrs_dip_opts, fixed at creation.
+        stream_priority: priority of the net's stream (torch.cuda.Stream; the engine's weight-gradient
+        side stream takes the same)."""
         import torch
 
         self.L = _lib.device_lib()
@@ -186,7 +188,7 @@ class DipNet:
             o = [ctypes.c_int64() for _ in range(4)]
             self.L.lrs_dipnet_param_offsets(h, i, *[ctypes.byref(x) for x in o])
             self.offsets.append(tuple(x.value for x in o))
-        self.stream = torch.cuda.Stream(device=device)
+        self.stream = torch.cuda.Stream(device=device, priority=int(stream_priority))
         self._es = None
 
     def __del__(self):
@@ -358,11 +360,12 @@ class DipProx:
     with skip()); one network object reused across outer iterations (re-initialised each call,
     as the reference builds a fresh net per call)."""
 
-    def __init__(self, bands: int, H: int, W: int, cfg: DipConfig | None = None, device="cuda"):
+    def __init__(self, bands: int, H: int, W: int, cfg: DipConfig | None = None, device="cuda",
+                 stream_priority: int = 0):
         self.cfg = cfg or DipConfig()
         nodes = (skip_nodes(bands, bands) if self.cfg.net == "skip"
                  else lipschitz_unet_nodes(bands, bands, self.cfg.hidden))
-        self.net = DipNet(nodes, bands, H, W, device=device)
+        self.net = DipNet(nodes, bands, H, W, device=device, stream_priority=stream_priority)
         if self.net.out_shape != (bands, H, W):
             raise ValueError(f"the DIP net maps {H}x{W} to {self.net.out_shape[1:]}; the reference "
                              "architecture needs sizes it reproduces (e.g. 36, 196 for the U-Net)")

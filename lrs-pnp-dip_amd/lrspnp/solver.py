@@ -49,6 +49,11 @@ class LrsPnPConfig:
     # 1 -> 7.50 outer it/s, 4 -> 7.49, 10 -> 7.39-7.42, 25 -> 7.27 (each slice re-forms D^T(m.*y) and
     # Phi, and runs longer beside the DIP than its share of one launch), so one launch.
     ista_slices_dip: int = 1
+    # Priority of the low-rank stream (torch.cuda.Stream priority: 0 = default, negative = higher).
+    # Beside the DIP, the sparse-coding kernel's resident workgroups can hold off a 1024-thread
+    # BatchNorm workgroup of the DIP for milliseconds; a higher-priority queue asks the dispatcher to
+    # place the DIP's workgroups first.
+    lowrank_priority: int = 0
 
     @staticmethod
     def dip_1lip(**kw) -> "LrsPnPConfig":
@@ -148,7 +153,7 @@ class LrsPnP:
         self.phi = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
         self.ista_ws = ops.ista_workspace(n, self.K, self.prox, dev)
         self.norms = torch.zeros(3, dtype=torch.float64, device=dev)
-        self.lowrank_stream = torch.cuda.Stream(device=dev)
+        self.lowrank_stream = torch.cuda.Stream(device=dev, priority=int(cfg.lowrank_priority))
         self.iteration = 0
         self.dip = None
         if comm is not None and (cfg.lowrank != "svt" or cfg.svt_method != "tri"):
@@ -171,7 +176,8 @@ class LrsPnP:
         if H * W != self.P:
             raise LrsError(f"image_shape {H}x{W} does not match P = {self.P}")
         self.H, self.W = H, W
-        self.dip = LipschitzDip(self.B, H, W, self.cfg.dip or DipConfig(), device=dev) if engine else None
+        self.dip = LipschitzDip(self.B, H, W, self.cfg.dip or DipConfig(), device=dev,
+                                 stream_priority=self.cfg.lowrank_priority) if engine else None
         self.dip_target = torch.empty((self.B, H, W), dtype=torch.float32, device=dev)
         ops.unfolded_to_image(self.Y, None, 1.0, H, W, self.dip_target)
         pix = ops.unfolded_to_image(self.M[:, :1].contiguous(), None, 1.0, H, W)   # (1, H, W)
