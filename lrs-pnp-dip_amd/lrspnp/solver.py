@@ -52,7 +52,8 @@ class LrsPnPConfig:
     # Priority of the low-rank stream (torch.cuda.Stream priority: 0 = default, negative = higher).
     # Beside the DIP, the sparse-coding kernel's resident workgroups can hold off a 1024-thread
     # BatchNorm workgroup of the DIP for milliseconds; a higher-priority queue asks the dispatcher to
-    # place the DIP's workgroups first.
+    # place the DIP's workgroups first.  Measured at configs[2] (bench.py --lowrank-priority, 2
+    # alternating rounds): 0 -> 7.43 / 7.43 outer it/s, -1 -> 7.48 / 7.41: no effect, so 0.
     lowrank_priority: int = 0
 
     @staticmethod

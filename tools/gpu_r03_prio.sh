@@ -10,7 +10,7 @@ for r in 1 2; do
     python -c "import json,sys; d=json.load(open('$o/b_${p}_$r.json')); print('prio $p run $r', d['value'], d['ms_per_step'])"
   done
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 --lowrank-priority -1 > $o/prof.log 2>&1 || { tail $o/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 --lowrank-priority -1 > $o/prof.log 2>&1 || { tail $o/prof.log; exit 1; }
 f=$(find $o/prof -name '*kernel_stats.csv' | head -n 1)
 cp "$f" $o/dip_kernel_stats_prio.csv
 python - <<'EOF'
