@@ -276,3 +276,30 @@ def test_task_parallel_dip_matches_one_rank(gpu, world):
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert r["world"] == world
     assert r["rel_X"] < 1e-6 and r["rel_L1"] < 1e-6 and r["rel_L2"] < 1e-6 and r["rel_U"] < 1e-6, r
+
+
+def test_lowrank_priority_same_iterates(gpu):
+    """LrsPnPConfig.lowrank_priority only changes the queue priority of the DIP's streams (its
+    training stream and the engine's weight-gradient side stream, which takes the same priority),
+    not the arithmetic: two DIP solvers in one process, priority 0 and -1, same seeds, give the same
+    iterates (1e-6 relative L2, the task-parallel test's bar) after 2 outer iterations."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.data import mask_matrix, synthetic_cube, synthetic_dictionary, unfold
+    from lrspnp.dip import DipConfig
+    H, W, B, bb = 36, 36, 40, 12
+    obs, clean, mask = synthetic_cube(H, W, B, seed=5)
+    Y, M = unfold(obs), mask_matrix(mask, B)
+    Dct = synthetic_dictionary(bb * bb, 256, 0)
+    out = []
+    for prio in (0, -1):
+        cfg = LrsPnPConfig.dip_1lip(bb=bb, sliding=bb, Nit=10, lowrank_priority=prio,
+                                    dip=DipConfig(num_iter=5, early_stop=False))
+        s = LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
+        assert s.lowrank_stream.priority == prio and s.dip.net.stream.priority == prio
+        for _ in range(2):
+            s.step()
+        torch.cuda.synchronize()
+        out.append((s.X.clone(), s.U.clone()))
+    (X0, U0), (X1, U1) = out
+    assert float((X1 - X0).norm() / X0.norm()) < 1e-6
+    assert float((U1 - U0).norm() / U0.norm()) < 1e-6
