@@ -388,6 +388,13 @@ inline int fwd_split_target() {
     return v;
 }
 
+// Split target of the padded-domain data-gradient GEMMs whose split-K partials k_fold_pad sums
+// (every partial is re-read by the fold, as by the forward BN kernels above).
+inline int dgrad_split_target() {
+    static const int v = (int)std::max<int64_t>(1, std::min<int64_t>(512, tune_knob("LRS_DIP_DGRAD_SPLIT_WG", 512)));
+    return v;
+}
+
 template <class LA, class LB>
 int gemm_s3_conv(const LA &la, const LB &lb, float *C, const float *bias, const float *div, int M, int N, int K,
                  float *part, int64_t part_cap, hipStream_t st, int *nsplit_out = nullptr, int accum = 0,
@@ -443,7 +450,8 @@ int upc_dgrad(const ConvGeom &g, const float *gz, const __bf16 *wd, int Cout, fl
     const int Cop = r16(Cout), K = 16 * Cop, Qe = (g.Hs + 2) * (g.Ws + 2);
     int nsplit = 1;   // split-K partials are summed inside the fold
     int rc = gemm_s3_conv(LdPre{wd, (int64_t)g.Cin * K, K, g.Cin}, LdUpDgradTM{gz, Cout * g.Ho * g.Wo * 4, g, Cout, Cop, nullptr},
-                          gxe, nullptr, nullptr, g.Cin, Qe, K, part, part_cap, st, &nsplit);
+                          gxe, nullptr, nullptr, g.Cin, Qe, K, part, part_cap, st, &nsplit, 0,
+                          dgrad_split_target());
     if (rc) return rc;
     ConvGeom fg = g;
     fg.up = 0;
@@ -661,7 +669,7 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         int nsplit = 1;   // split-K partials are summed inside the fold
         rc = gemm_s3_conv(LdPre{wd, (int64_t)g.Cin * kk * Cop, kk * Cop, g.Cin},
                           LdDgradTM{gz, Cout * P * 4, g, Cout, Cop, nullptr}, dcol, nullptr, nullptr, g.Cin, Qp,
-                          kk * Cop, part, part_cap, st, &nsplit);
+                          kk * Cop, part, part_cap, st, &nsplit, 0, dgrad_split_target());
         if (rc) return rc;
         const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
         hipLaunchKernelGGL(k_fold_pad, grid, dim3(256), 0, st, nsplit > 1 ? part : dcol, nsplit, (int64_t)g.Cin * Qp, g,
