@@ -993,6 +993,8 @@ constexpr int kBnRegMaxQ = 10;   // 40960 pixels
 
 template <int NQ>
 __device__ __forceinline__ bool bnr_ok(int P, int u) { return threadIdx.x + u * kBn1Threads < (unsigned)(P >> 2); }
+template <int TH>
+__device__ __forceinline__ bool bnr_ok_t(int P, int u) { return threadIdx.x + u * TH < (unsigned)(P >> 2); }
 
 // quad q of a [C][P] tensor at channel offset off, summed over nsplit split-K partials (stride MN):
 // acc[e] = the splits e, e + 8, ... in increasing order (k_gemm_reduce's order); the loads of one
@@ -1023,8 +1025,10 @@ __device__ __forceinline__ float4 splitk_sum4(const float *__restrict__ part, in
 
 // forward: z = (split-K partials summed in k_gemm_reduce's order + bias) or z as stored; then
 // BN statistics, normalisation, affine (Lipschitz rescale), activation.  part == nullptr: z given.
-template <int NQ>
-__global__ __launch_bounds__(kBn1Threads) void k_bn_fwd_r(const float *__restrict__ part, int nsplit,
+// TH = threads per workgroup (quads t + TH u): 1024 by default; 256 (4 wave slots instead of 16) lets a
+// 98^2 map's workgroup fit where one sparse-coding workgroup retires (tuning build, LRS_DIP_BNR_SMALL_WG)
+template <int NQ, int TH = kBn1Threads>
+__global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part, int nsplit,
                                                           const float *__restrict__ bias, BnArgs a) {
     __shared__ double red[2 * kBn1Threads / 64];
     __shared__ float redf[kBn1Threads / 64];
@@ -1036,8 +1040,8 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd_r(const float *__restric
 #pragma unroll
     for (int u = 0; u < NQ; ++u) {
         zv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!bnr_ok<NQ>(a.P, u)) continue;
-        const int q = t + u * kBn1Threads;
+        if (!bnr_ok_t<TH>(a.P, u)) continue;
+        const int q = t + u * TH;
         if (!part) {
             zv[u] = z4[q];
             continue;
@@ -1058,7 +1062,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd_r(const float *__restric
     double s1 = 0.0, s2 = 0.0;
 #pragma unroll
     for (int u = 0; u < NQ; ++u)
-        if (bnr_ok<NQ>(a.P, u)) {
+        if (bnr_ok_t<TH>(a.P, u)) {
             const double d0 = (double)zv[u].x - K, d1 = (double)zv[u].y - K, d2 = (double)zv[u].z - K,
                          d3 = (double)zv[u].w - K;
             s1 += d0; s2 += d0 * d0;
@@ -1092,9 +1096,9 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd_r(const float *__restric
     float4 *y4 = reinterpret_cast<float4 *>(a.y + off);
 #pragma unroll
     for (int u = 0; u < NQ; ++u)
-        if (bnr_ok<NQ>(a.P, u)) {
+        if (bnr_ok_t<TH>(a.P, u)) {
             const float4 v = zv[u];
-            y4[t + u * kBn1Threads] =
+            y4[t + u * TH] =
                 make_float4(act_fwd((v.x - m32) * is32 * gm + bt, a.act), act_fwd((v.y - m32) * is32 * gm + bt, a.act),
                             act_fwd((v.z - m32) * is32 * gm + bt, a.act), act_fwd((v.w - m32) * is32 * gm + bt, a.act));
         }

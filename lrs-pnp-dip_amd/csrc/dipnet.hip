@@ -712,6 +712,12 @@ inline int bn_reg_q(int64_t P, bool vec) {
     return 0;
 }
 
+// 98^2 maps' register BN forward on 256-thread workgroups (tuning build only; default off)
+inline bool bnr_small_wg() {
+    static const bool v = tune_knob("LRS_DIP_BNR_SMALL_WG", 0) != 0;
+    return v;
+}
+
 #define LRS_BNR_SWITCH(nq, K, ...)                                                                \
     switch (nq) {                                                                                 \
     case 2: hipLaunchKernelGGL(K<2>, __VA_ARGS__); break;                                         \
@@ -1223,8 +1229,12 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
                                net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C, nullptr, N.C,
                                (int)N.P, 1, (int)N.P, 1, N.d.act, 1e-5f, 0.1f, lip, 1};
                 const float *pp = nsplit > 1 ? (const float *)net->f(net->part_off) : nullptr;
-                LRS_BNR_SWITCH(nq, k_bn_fwd_r, dim3(1, N.C), dim3(kBn1Threads), 0, st, pp, nsplit,
-                               (const float *)(net->params + N.b_off), a);
+                if (bnr_small_wg() && nq == 3 && N.P <= 4 * 256 * 10)
+                    hipLaunchKernelGGL((k_bn_fwd_r<10, 256>), dim3(1, N.C), dim3(256), 0, st, pp, nsplit,
+                                       (const float *)(net->params + N.b_off), a);
+                else
+                    LRS_BNR_SWITCH(nq, k_bn_fwd_r, dim3(1, N.C), dim3(kBn1Threads), 0, st, pp, nsplit,
+                                   (const float *)(net->params + N.b_off), a);
                 rc = LRS_OK;
             } else if (fuse && nsplit > 1) {
                 const BnArgs a{z, out, net->params + N.gm_off, net->params + N.bt_off, net->f(N.mean_off),
