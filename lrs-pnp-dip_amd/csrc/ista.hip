@@ -1204,9 +1204,30 @@ __global__ __launch_bounds__(256) void k_nlm_col(const float *__restrict__ g, in
     }
 }
 
+// k_nlm_col's dynamic LDS is (K + 10) floats: above 64 KiB (K > 16374) the launch must be opted into
+// more (gfx950: 160 KiB per workgroup).  Set once per process.
+static int nlm_col_lds(int64_t K) {
+    const size_t bytes = (size_t)(K + 10) * sizeof(float);
+    static bool opted = false;
+    if (bytes > 65536 && !opted) {
+        const hipError_t e = hipFuncSetAttribute((const void *)k_nlm_col, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024);
+        if (e != hipSuccess) return (int)e;
+        opted = true;
+    }
+    return LRS_OK;
+}
+
 }  // namespace lrs
 
 using namespace lrs;
+
+// k_ista_ln2's quotient: 2 = one Newton step on v_rcp_f64 plus a remainder correction, 1 = the Newton
+// step alone.  Both are < 1 ulp of fp64 before the float rounding; the register allocation of this
+// VGPR-saturated kernel is what differs.
+#ifndef LRS_LN2_DIV
+#define LRS_LN2_DIV 1
+#endif
 
 // row-split kernel (csrc/ista_rs.hip): any n, K <= 512, every prox
 namespace lrs {
@@ -1314,6 +1335,8 @@ int ista_generic(const float *Yb, const uint8_t *obs, const float *D, int64_t n,
                 rc = nlm_matlab_col_launch(G, K, X, K, K, rows, 0.0, thr + j0, st);
                 if (rc) return rc;
             } else {
+                rc = nlm_col_lds(K);
+                if (rc) return rc;
                 hipLaunchKernelGGL(k_nlm_col, dim3((unsigned)rows), dim3(256), (size_t)(K + 10) * sizeof(float), st, G,
                                    K, X, K, (int)K, 0.0, thr + j0);
             }
@@ -1367,10 +1390,12 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     if (n_pad > (int64_t)1 << 20 || nb > ((int64_t)1 << 40)) return LRS_E_INVALID;
     if (nb == 0) return LRS_OK;
     hipStream_t st = (hipStream_t)stream;
-    if (ista_use_generic(K, opts))
-        return ista_generic(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, st);
+    // warm start exists only on the row-split kernel: refuse it before any dispatch (the generic path
+    // would otherwise restart from zero on every slice)
     const bool warm = opts && opts->warm_start;
     if (warm && (!coefs || ista_use_generic(K, opts) || ista_resident(n_pad, K, prox))) return LRS_E_UNSUPPORTED;
+    if (ista_use_generic(K, opts))
+        return ista_generic(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, st);
     if (!ista_resident(n_pad, K, prox))
         return ista_rs_launch(Yb, obs, D, n, n_pad, K, nb, alpha, thr, Nit, prox, coefs, phi, ws, ws_bytes, max_wg, st,
                               warm ? coefs : nullptr);
@@ -1382,7 +1407,7 @@ extern "C" int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D,
     if (split && prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_b3<256, true>), grid_b3, dim3(kB3Threads), 0, st, p);
     else if (split)
-        hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, 1>), grid_b3, dim3(kB3Threads), 0, st, p);
+        hipLaunchKernelGGL((k_ista_ln2<256, false, 1, true, LRS_LN2_DIV>), grid_b3, dim3(kB3Threads), 0, st, p);
     else if (prox == LRS_PROX_SOFT)
         hipLaunchKernelGGL((k_ista_res<256, true>), grid, dim3(kIstaThreads), 0, st, p);
     else
@@ -1398,6 +1423,8 @@ extern "C" int lrs_nlm_col_f32(const float *g, int64_t ldg, float *out, int64_t 
     if (patch_size != 3 || patch_distance != 3) return LRS_E_UNSUPPORTED;
     if (K > 16384) return LRS_E_UNSUPPORTED;
     if (nvec == 0) return LRS_OK;
+    const int rc = nlm_col_lds(K);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_nlm_col, dim3((unsigned)nvec), dim3(256), (size_t)(K + 10) * sizeof(float),
                        (hipStream_t)stream, g, ldg, out, ldo, (int)K, h, h_per_vec);
     LRS_CHECK_LAUNCH();

@@ -253,8 +253,16 @@ class DipTaskSplit:
             lr = s.lowrank_stream
             lr.wait_stream(main)
             comm.wait_stream(main)
-            parts = self._gather_phi(comm)        # beside the DIP (nccl): rank 0 contributes no rows
-            s.low_rank_dip(lr)
+            if dist.get_backend() == "nccl":
+                # the RCCL all-gather is enqueued first so it runs beside the DIP training (rank 0
+                # contributes no rows); the multi-rank overlap is unmeasured on hardware
+                parts = self._gather_phi(comm)
+                s.low_rank_dip(lr)
+            else:
+                # gloo's gather blocks the host until the workers finish: train the DIP first, so it
+                # still overlaps the workers' sparse coding
+                s.low_rank_dip(lr)
+                parts = self._gather_phi(comm)
             comm.wait_stream(lr)
         else:
             b0, b1 = self.ranges[ctx.rank]

@@ -272,6 +272,7 @@ class LrsPnpOracle:
         self.bb, self.sliding = bb, sliding
         self.gamma, self.mu1, self.mu2 = gamma, mu1, mu2
         self.Nit, self.variant = Nit, variant
+        self.lowrank = lowrank
         self.prox = {"soft": PROX_SOFT, "matlab": PROX_NLM_MATLAB}.get(variant, PROX_NLM)
         self.rows, self.cols = block_grid(self.P, self.B, bb, sliding)
         self.nb = self.rows.size
@@ -297,7 +298,9 @@ class LrsPnpOracle:
         blocks = im2col(Xsc, self.bb, self.rows, self.cols)
         _, PHI = ista_batch(blocks, self.obs, self.D, self.alpha, self.thr, self.Nit, self.prox)
         Xlr = self.X + f32(1 / self.mu2) * self.L2                     # :315
-        U = svt(Xlr, 1 / self.mu2)
+        # low-rank prox: the SVT (:315), or a callable standing for the DIP mains' get_DIP_out on
+        # (X + L2/mu2) (main_LRS_PnP_DIP_1-LiP.py:399-411; tests/golden/gen_dip196_traj.py)
+        U = self.lowrank(Xlr) if callable(self.lowrank) else svt(Xlr, 1 / self.mu2)
         Xn, L1n, L2n = (np.empty_like(self.X) for _ in range(3))
         IM = np.empty_like(self.X)
         lib().oracle_admm_update(self.P, self.B, self.bb, self.nb, self.rows, self.cols,

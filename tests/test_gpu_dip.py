@@ -390,6 +390,82 @@ def test_unet_gradients_implicit_sizes_vs_fp64(L, upsample_dgrad):
             assert rel(gg, gr) < max(1e-4, 2 * rel(g32, gr)) and rel(beg, ber) < max(1e-4, 2 * rel(be32, ber)), i
 
 
+def _grads_vs_fp64_on_gpu(nodes, flat, x, t, m, net, c0, H, W):
+    """Step-0 gradient of the engine against the restatement in fp64 and fp32 torch on the GPU (TF32
+    off): per parameter tensor, (engine error, fp32-torch error) relative to fp64."""
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    grads = {}
+    for dt in (torch.float64, torch.float32):
+        p = flat.to(dt).cuda().clone().requires_grad_(True)
+        dip_ref.loss_fn(dip_ref.forward(p, nodes, x.to(dt).cuda()), t.to(dt).cuda(), m.to(dt).cuda()).backward()
+        grads[dt] = p.grad.double().cpu()
+        del p
+    net.train_steps(x.cuda(), t.cuda(), m.cuda(), 1, use_graph=False)
+    torch.cuda.synchronize()
+    gd = net.grads.cpu().double()
+    offs, _ = dip_ref.param_offsets(nodes, c0, H, W)
+    out = []
+    for i in range(len(nodes)):
+        trip = zip(dip_ref.views(gd, nodes, i, offs, c0, H, W), dip_ref.views(grads[torch.float64], nodes, i, offs, c0, H, W),
+                   dip_ref.views(grads[torch.float32], nodes, i, offs, c0, H, W))
+        for j, (ga, g64, g32) in enumerate(trip):
+            if ga is not None:
+                out.append((i, j, rel(ga, g64), rel(g32, g64)))
+    return out
+
+
+def test_unet_gradients_bench_size_196_vs_fp64(L):
+    """BASELINE configs[2]'s DIP at its benched size: the 198 -> 128 -> 198 my_Lipschitz_Unet on
+    196 x 196 (models/my_Lipschitz_Unet.py:116-148; its 196^2 / 98^2 maps run the register-resident
+    BatchNorm k_bn_fwd_r / k_bn_bwd_r, the parity-class upsampled convs LdUpDgradTM / LdWgradCls +
+    k_upc_wgrad_combine, k_fold_pad and the weight-gradient side stream).  Step-0 gradients of every
+    parameter tensor against the fp64 restatement on the GPU: 1e-4 relative, or twice the fp32-torch
+    error where fp32 itself is further from fp64 (as at 36^2 and 52^2).  Biases feeding a BN are
+    rounding noise in exact arithmetic (fp32 error > 100 %) and skipped."""
+    from gen_dip_golden import flat_params
+    from lrspnp.dip import lipschitz_unet_units
+    C, H = 198, 196
+    units = lipschitz_unet_units(C, C, 128)
+    flat = torch.from_numpy(flat_params(units, 41, C, H, H))
+    g = torch.Generator().manual_seed(12)
+    x, t = torch.rand(C, H, H, generator=g), torch.rand(C, H, H, generator=g)
+    m = (torch.rand(H * H, generator=g) > 0.1).float()
+    net = _engine(units, flat, H, H, C)
+    res = _grads_vs_fp64_on_gpu(units, flat, x, t, m, net, C, H, H)
+    worst = max(res, key=lambda r: r[2] / max(1e-4, 2 * r[3]) if r[3] <= 1.0 else 0)
+    print("worst (node, tensor, engine err, fp32 err):", worst)
+    for i, j, e, e32 in res:
+        if e32 > 1.0:
+            continue
+        assert e < max(1e-4, 2 * e32), (i, j, e, e32)
+
+
+def test_skip_net_gradients_config3_size_vs_fp64(L):
+    """BASELINE configs[3]'s DIP at full size: the skip net on 512 x 512 x 224 (models/skip.py:5-99,
+    main_LRS_PnP_DIP_pro.py:215-221).  Step-0 gradients against the fp64 restatement on the GPU with
+    the bound of the 36^2 skip test: at most twice the fp32-torch error, and 2e-3 elsewhere (BN over
+    the deep 32^2..16^2 maps conditions these gradients; a pre-activation within rounding of 0 may
+    take the other LeakyReLU branch).  Entries that are rounding noise in exact arithmetic are
+    skipped."""
+    from gen_dip_golden import flat_params
+    from lrspnp.dip import skip_nodes
+    C, H = 224, 512
+    nodes = skip_nodes(C, C)
+    flat = torch.from_numpy(flat_params(nodes, 13, C, H, H))
+    g = torch.Generator().manual_seed(4)
+    x, t = torch.rand(C, H, H, generator=g), torch.rand(C, H, H, generator=g)
+    m = (torch.rand(H * H, generator=g) > 0.05).float()
+    net = _engine(nodes, flat, H, H, C)
+    res = _grads_vs_fp64_on_gpu(nodes, flat, x, t, m, net, C, H, H)
+    worst = max(res, key=lambda r: r[2] / max(2e-3, 2 * r[3]) if r[3] <= 1.0 else 0)
+    print("worst (node, tensor, engine err, fp32 err):", worst)
+    for i, j, e, e32 in res:
+        if e32 > 1.0:
+            continue
+        assert e < max(2e-3, 2 * e32), (i, j, e, e32)
+
+
 def test_nets_with_different_opts_coexist(L):
     """Per-handle modes (lrs_dip_opts, fixed at creation; no process-wide state): a split-bf16 and an
     f32 net, and a zero-padded U-Net (its upsampled convs take the effective-kernel data gradient
@@ -576,7 +652,8 @@ def test_skip_net_forward_step_vs_reference(L, golden):
 
 
 def test_skip_net_generalised_bands(L):
-    """skip net at 200 x 200 x 198 (any H, W: Concat crops)."""
+    """skip net with 198 bands on a ragged 50 x 44 map (any H, W: Concat crops; SURVEY.md §8 a12);
+    the literal 200 x 200 x 198 size is test_skip_net_literal_config2_cube."""
     from gen_dip_golden import flat_params
     from lrspnp.dip import skip_nodes
     nodes = skip_nodes(198, 198)
@@ -586,6 +663,31 @@ def test_skip_net_generalised_bands(L):
     out = net.forward(x.cuda()).cpu()
     assert out.shape == (198, 50, 44)
     assert rel(out, dip_ref.forward(flat, nodes, x)) < 1e-5
+
+
+def test_skip_net_literal_config2_cube(L):
+    """The skip net on BASELINE configs[2]'s literal 200 x 200 x 198 cube (bench.py --workload dip-pro
+    --cube 200x200x198): forward vs the fp32 restatement on the GPU at 1e-5, step-0 loss at 1e-5."""
+    from gen_dip_golden import flat_params
+    from lrspnp.dip import skip_nodes
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    C, H = 198, 200
+    nodes = skip_nodes(C, C)
+    flat = torch.from_numpy(flat_params(nodes, 17, C, H, H))
+    g = torch.Generator().manual_seed(6)
+    x, t = torch.rand(C, H, H, generator=g), torch.rand(C, H, H, generator=g)
+    m = (torch.rand(H * H, generator=g) > 0.05).float()
+    net = _engine(nodes, flat, H, H, C)
+    out = net.forward(x.cuda())
+    with torch.no_grad():
+        ref = dip_ref.forward(flat.cuda(), nodes, x.cuda())
+        loss_r = float(dip_ref.loss_fn(ref, t.cuda(), m.cuda()))
+    assert out.shape == ref.shape == (C, H, H)
+    assert rel(out, ref) < 1e-5
+    net.train_steps(x.cuda(), t.cuda(), m.cuda(), 1, use_graph=False)
+    torch.cuda.synchronize()
+    assert abs(net.last_loss() - loss_r) < 1e-5 * loss_r
 
 
 def test_skip_net_config3_full_size(L):

@@ -60,3 +60,38 @@ def test_dip_main_quality_within_reference_band(gpu, golden, net):
     assert np.all(np.abs(smean - RS.mean(0)) <= bound(GS, RS, 0.005)), (smean, RS.mean(0), bound(GS, RS, 0.005))
     # the reference's outer loop improves the cube every iteration; so must this one
     assert np.all(np.diff(mean) > 0)
+
+
+def test_dip196_trajectory_vs_oracle_restatement(gpu, golden):
+    """BASELINE configs[2] as benched (bench.py --workload dip: the seeded 196 x 196 x 198 cube, 36 x 36
+    blocks, fro4 ISTA Nit 100, the 198 -> 128 -> 198 my_Lipschitz_Unet DIP, 100 Adam steps per outer
+    iteration, early stopping off) against the oracle-driven restatement of the same outer loop
+    (tests/golden/gen_dip196_traj.py: the C ISTA, oracle/dip_ref.py's torch U-Net with full-SVD
+    sigma_max and torch Adam, the C X / dual update; the reference main itself cannot run 198 bands).
+    Per outer iteration, the mean MPSNR over the GPU's seeds equals the restatement's mean over its
+    seeds within three standard errors of the difference + 0.01 dB (the rule of the 36 x 36 test)."""
+    from lrspnp import LrsPnP, LrsPnPConfig
+    from lrspnp.data import load_fixture, mask_matrix, synthetic_cube, synthetic_dictionary, unfold
+    from lrspnp.dip import DipConfig
+    from lrspnp.metrics import mpsnr
+    ref = golden("dip196_traj_ref.npz")
+    R = ref["mpsnr"]                                   # (seeds, iterations)
+    iters = R.shape[1]
+    H, W, B = 196, 196, 198
+    obs, clean, mask = synthetic_cube(H, W, B, seed=0, base_mask=load_fixture("data_img5.npz")["lrs_mask"])
+    Y, M, D = unfold(obs), mask_matrix(mask, B), synthetic_dictionary(36 * 36, 256, 0)
+    clean_d = torch.from_numpy(clean).cuda()
+    nseed = 8
+    G = np.empty((nseed, iters))
+    for seed in range(nseed):
+        cfg = LrsPnPConfig.dip_1lip(dip=DipConfig(num_iter=100, early_stop=False), dip_seed=1000 * seed)
+        s = LrsPnP(Y, M, D, cfg, image_shape=(H, W))
+        if seed == 0:
+            assert abs(mpsnr(s.X, clean_d) - float(ref["mpsnr_input"])) < 1e-6
+        for it in range(iters):
+            s.step()
+            G[seed, it] = mpsnr(s.X, clean_d)
+    mean = G.mean(0)
+    bound = 3.0 * np.sqrt(G.var(0, ddof=1) / nseed + R.var(0, ddof=1) / len(R)) + 0.01
+    print("GPU", np.round(mean, 4), "restatement", np.round(R.mean(0), 4), "bound", np.round(bound, 4))
+    assert np.all(np.abs(mean - R.mean(0)) <= bound), (mean, R.mean(0), bound)

@@ -213,6 +213,33 @@ def test_ista_warm_start_slices_are_one_launch(ops, K, prox):
     assert torch.equal(phi, phi1) and torch.equal(co, co1)
     with pytest.raises(LrsError):
         ops.ista(*args, 2, pr, warm_start=True)
+    # warm start exists only on the row-split kernel: the generic dense-GEMM path (algorithm 1, or
+    # K > 512) refuses it instead of silently restarting from zero
+    with pytest.raises(LrsError):
+        ops.ista(*args, 2, pr, coefs=co, want_coefs=True, warm_start=True, algorithm=1)
+
+
+def test_ista_warm_start_refused_above_k512(ops):
+    from lrspnp.data import synthetic_dictionary
+    from lrspnp._lib import LrsError
+    rng = np.random.default_rng(6)
+    n, nb, K = 8 * 8, 20, 768
+    D = synthetic_dictionary(n, K, seed=4)
+    Yb, obs = _rand_blocks(rng, nb, n, 0.2)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    co = torch.zeros((nb, K), device="cuda")
+    with pytest.raises(LrsError):
+        ops.ista(d(Yb), d(obs), d(D), n, d(np.ones(nb, np.float32)), d(np.full(nb, 0.05)), 2, ops.PROX_NLM,
+                 coefs=co, want_coefs=True, warm_start=True)
+
+
+def test_nlm_col_top_of_k_range(ops):
+    """k_nlm_col at the documented top of its range, K = 16384: (K + 10) floats of LDS exceed
+    64 KiB and the launch is opted into more; bit-exact vs the oracle like every other K."""
+    g = np.random.default_rng(3).uniform(0, 1, (2, 16384)).astype(np.float32)
+    out = ops.nlm_col(torch.from_numpy(g).cuda(), 0.04).cpu().numpy()
+    for v in range(2):
+        np.testing.assert_array_equal(out[v], O.nlm_col(g[v], 0.04))
 
 
 def test_ista_kernel_vs_reference_golden(ops, golden):
