@@ -28,7 +28,9 @@ Rank 0 prints one JSON line with
   roofline     : the dominant stage — the DIP training of one outer iteration (dip workloads) or
                  the ISTA kernel (pnp): algorithmic MFMA FLOPs / time from HIP events on the stream
                  it runs on, vs the 157.3 TFLOP/s f32 MFMA peak; `traffic` = HBM bytes from the
-                 committed rocprofv3 PMC pass (profiles/r02/traffic.json), per the same unit.
+                 committed rocprofv3 PMC pass (profiles/r04/traffic.json), per the same unit;
+                 `peak_split_bf16` / `frac_split_bf16`: the same work against the split-bf16
+                 matrix-core ceiling (6 bf16 MFMAs per fp32-accurate product).
                  `roofline.kernels` adds the sparse-coding kernel (k_ista_rs / k_ista_ln2) per launch.
   cpu_baseline : the oracle timed on this host (rank 0, N = 1): the C ISTA restatement on a bounded
                  block sample + (dip) the plain-torch DIP restatement (oracle/dip_ref.py) for a few
@@ -52,7 +54,12 @@ import numpy as np  # noqa: E402
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table (f32 MFMA = f32 vector peak)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03", "traffic.json")
+# The split-bf16 kernels (the DIP convs, k_ista_ln2) compute each fp32-accurate product as 6
+# v_mfma_f32_16x16x32_bf16 (16 cycles per SIMD each, MI355X_MICROARCH.md cycle constants): 1024 FLOP
+# per clock per SIMD x 4 x 256 CUs x 2.4 GHz = 2,517 TFLOP/s of bf16, / 6 = the ceiling of fp32-accurate
+# work on the bf16 matrix cores.
+SPLIT_BF16_PEAK_TFLOPS = 2516.6 / 6
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r04", "traffic.json")
 
 
 def parse():
@@ -114,7 +121,7 @@ def make_problem(H, W, B, bb, K, seed):
 
 
 def load_traffic(key, profiled=True):
-    """HBM bytes of the committed PMC pass (profiles/r03/traffic.json); None for a configuration
+    """HBM bytes of the committed PMC pass (profiles/r04/traffic.json); None for a configuration
     other than the profiled default one."""
     if not profiled:
         return None
@@ -357,7 +364,9 @@ def main_dip(args, ctx):
         "vs_baseline": None, "dtype": "f32 (MFMA products fp32-accurate) + f64 (NLM prox, BN/sigma statistics)",
         "data": f"synthetic (seeded low-rank {H}x{W}x{B} cube per rank, tiled low_rank_sparsity_mask, seeded "
                 f"K={args.K} dictionary, random-init DIP net per outer iteration)",
-        "config": {"workload": (f"LRS-PnP-DIP(pro) {H}x{W}x{B} (BASELINE configs[3]; configs[4] = one such cube per "
+        "config": {"workload": (f"LRS-PnP-DIP(pro) skip net on the literal {H}x{W}x{B} cube (BASELINE configs[2] "
+                                f"as written; the skip net maps any H x W)" if pro and (H, W, B) == (200, 200, 198) else
+                                f"LRS-PnP-DIP(pro) {H}x{W}x{B} (BASELINE configs[3]; configs[4] = one such cube per "
                                 f"GPU)" if pro else
                                 f"LRS-PnP-DIP(1-Lip) on a {H}x{W}x{B} cube" if args.cube else
                                 f"LRS-PnP-DIP(1-Lip) on the 200x200x198 cube cropped to {H}x{W}x{B} "
@@ -371,6 +380,9 @@ def main_dip(args, ctx):
                                                 f"GEMMs, sigma_max, BN, loss, Adam kernels)",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                     # the convs run on the bf16 matrix cores, 6 MFMAs per fp32-accurate product
+                     "peak_split_bf16": SPLIT_BF16_PEAK_TFLOPS,
+                     "frac_split_bf16": achieved / SPLIT_BF16_PEAK_TFLOPS,
                      "traffic": traffic,
                      "alg_bytes": alg_bytes,
                      "traffic_over_alg": (traffic / alg_bytes) if traffic and alg_bytes else None,
@@ -433,6 +445,9 @@ def main_pnp(args, ctx):
     entry = ista_entry("k_ista_ln2 (lrs_ista_f32)", ista_t.mean_ms(), flops, "pnp_ista_hbm_bytes_per_launch")
     roof = {k: entry[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
                                   "flops_per_launch", "ms_per_launch")}
+    # k_ista_ln2's products are split-bf16 (6 bf16 MFMAs each); its NLM prox is fp64 VALU
+    roof["peak_split_bf16"] = SPLIT_BF16_PEAK_TFLOPS
+    roof["frac_split_bf16"] = entry["achieved"] / SPLIT_BF16_PEAK_TFLOPS
     out = {
         "metric": METRIC, "value": (1 if split else world) * args.steps / elapsed, "unit": "outer_iters/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
