@@ -1170,6 +1170,14 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln2(IstaParams p) {
     }
 }
 
+// A second instantiation of k_ista_ln2 (the DIV = 0 quotient, never launched) beside the product's
+// <256, false, 1, true, 1>: with it the product kernel compiles to exactly round 1's code (30 AGPRs,
+// 104 v_accvgpr moves); compiled alone, the same source gets 82 AGPRs and 241 moves, and configs[1]
+// loses 2.8 % (k_ista_ln2 7.88 vs 7.59 ms per launch; profiles/r04/ab_pnp).  LLVM's inlining of the
+// shared helpers depends on how many kernels call them, and with it the register allocation of this
+// VGPR-saturated kernel.
+template __global__ void k_ista_ln2<256, false, 1, true, 0>(IstaParams);
+
 // Standalone NLM over nvec columns of length K (any K >= 1): one workgroup per column, the
 // column reflect-padded in LDS, one thread per output.  Used by lrs_nlm_col_f32 (the
 // denoise_nl_means drop-in) — the fused ISTA kernel above does not call it.

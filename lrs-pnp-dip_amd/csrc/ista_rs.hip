@@ -27,6 +27,10 @@
 // Products use v_mfma_f32_16x16x4_f32 (exact f32 products; f32 accumulation in MFMA order).
 // A ring of 8 float4 keeps the next 8 dictionary fragments in flight across the product and
 // row-tile boundaries.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "lrs_common.h"
 #include "lrs_nlm.h"
 
@@ -474,7 +478,13 @@ static int launch_rs_k(const IstaRsParams &p, int64_t max_wg, hipStream_t st) {
         if (e != hipSuccess) return (int)e;
         lds_opt_in = true;
     }
-    hipLaunchKernelGGL((k_ista_rs<NQ, MINW, S>), dim3((unsigned)tiles), dim3(64 * S), rs_lds_bytes(NQ, S), st, p);
+    size_t lds = rs_lds_bytes(NQ, S);
+#ifdef LRS_TUNING
+    // A/B only: LRS_ISTA_RS_LDS = dynamic LDS per workgroup (bytes, >= the kernel's), e.g. 98304 holds
+    // the sparse coding to one workgroup per CU beside the DIP
+    if (const char *e = getenv("LRS_ISTA_RS_LDS")) lds = std::max<size_t>(lds, (size_t)atoll(e));
+#endif
+    hipLaunchKernelGGL((k_ista_rs<NQ, MINW, S>), dim3((unsigned)tiles), dim3(64 * S), lds, st, p);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }

@@ -3,7 +3,7 @@
 # 1c05b02 by tools/build_ab_r01.sh) against HEAD, interleaved 3 times; k_ista_ln2 from a kernel trace of each.
 set -o pipefail
 export TMPDIR=/tmp
-o=gpurun_out/ab_pnp
+o=gpurun_out/r04d/ab_pnp
 mkdir -p $o
 for rnd in 1 2 3; do
   (cd ab_r01 && timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline) > $o/r01_$rnd.json 2> $o/r01.err || { tail $o/r01.err; exit 1; }
