@@ -33,3 +33,7 @@ for k, d in acc.items():
 PY
   done
 done
+for r in 1 2; do
+  timeout -k 10 200 python bench.py --workload pnp --steps 20 --warmup 3 --no-cpu-baseline > $o/pnp_$r.json 2> $o/pnp_$r.err || { tail $o/pnp_$r.err; exit 1; }
+  python -c "import json; d=json.loads(open('$o/pnp_$r.json').read().strip().splitlines()[-1]); print('pnp run $r', round(d['value'],2), d['roofline']['ms_per_launch'])"
+done
