@@ -80,6 +80,10 @@ def parse():
                     help="workgroups of the sparse-coding kernel beside the DIP (default LrsPnPConfig's; 0 = unbounded)")
     ap.add_argument("--lowrank-priority", type=int, default=None,
                     help="priority of the low-rank (DIP) stream (LrsPnPConfig.lowrank_priority; negative = higher)")
+    ap.add_argument("--ista-dip-order", default=None, choices=["beside", "before"],
+                    help="DIP workloads: sparse coding beside the DIP training or before it (LrsPnPConfig.ista_dip_order)")
+    ap.add_argument("--ista-patterns", default=None, choices=["auto", "on", "off"],
+                    help="sparse coding on per-pattern masked Grams (LrsPnPConfig.ista_patterns)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group: nccl (= RCCL, one GPU per rank) or gloo (rehearsal: rank r on GPU "
@@ -318,6 +322,10 @@ def main_dip(args, ctx):
         extra["ista_slices_dip"] = args.ista_slices
     if args.lowrank_priority is not None:
         extra["lowrank_priority"] = args.lowrank_priority
+    if args.ista_dip_order is not None:
+        extra["ista_dip_order"] = args.ista_dip_order
+    if args.ista_patterns is not None:
+        extra["ista_patterns"] = args.ista_patterns
     cfg = (LrsPnPConfig.dip_pro if pro else LrsPnPConfig.dip_1lip)(bb=bb, sliding=bb, Nit=nit, dip=dcfg, **extra)
     task = D.DipTaskSplit(Y, M, Dct, cfg, ctx, image_shape=(H, W)) if split else None
     s = task.s if split else LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
@@ -326,8 +334,9 @@ def main_dip(args, ctx):
 
     dip_t, ista_t = StreamTimer(), StreamTimer()
     s.low_rank_dip = dip_t.wrap(s.low_rank_dip, lambda a, k: a[0])
-    orig_ista = ops.ista
+    orig_ista, orig_ista_pat = ops.ista, ops.ista_pat
     ops.ista = ista_t.wrap(orig_ista, lambda a, k: k.get("stream") or torch.cuda.current_stream())
+    ops.ista_pat = ista_t.wrap(orig_ista_pat, lambda a, k: k.get("stream") or torch.cuda.current_stream())
     count = [0]
 
     def step():
@@ -336,7 +345,7 @@ def main_dip(args, ctx):
         (task.step if split else s.step)()
 
     elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
-    ops.ista = orig_ista
+    ops.ista, ops.ista_pat = orig_ista, orig_ista_pat
     mp1 = mpsnr(s.X, clean_d)
     # a time-sliced sparse coding (LrsPnPConfig.ista_slices_dip) is several back-to-back launches:
     # its time per outer iteration is their sum
@@ -352,7 +361,14 @@ def main_dip(args, ctx):
     profiled = not (args.cube or args.bb or args.nit or args.K != 256 or args.dip_steps != 100)
     achieved = flops / (dip_ms * 1e-3) / 1e12
     n = bb * bb
-    ista_flops = nit * s.nb * 4 * n * args.K + s.nb * 2 * n * args.K
+    pat = getattr(s, "pat_plan", None) is not None
+    # matrix-core work per launch: the row-split kernel's two products per iteration (+ Phi), or the
+    # per-pattern path's Grams, b and Phi once and one K x K product per iteration
+    ista_flops = (s.npat * 2 * n * args.K ** 2 + s.nb * (4 * n * args.K + nit * 2 * args.K ** 2) if pat else
+                  nit * s.nb * 4 * n * args.K + s.nb * 2 * n * args.K)
+    ista_name = (f"k_ista_pat (lrs_ista_pat_f32: {s.nb} blocks of {n} rows in {s.pat_ntiles} tiles of "
+                 f"{s.npat} observation patterns, Nit {nit}" if pat else
+                 f"k_ista_rs (lrs_ista_f32: {s.nb} blocks of {n} rows, Nit {nit}")
     net_desc = ("skip net (5 x 128 ch, 128-ch skips)" if pro else f"my_Lipschitz_Unet ({B}->128->{B} ch)")
     tag = "dip_pro" if pro else "dip"
     traffic = load_traffic(f"{tag}_hbm_bytes_per_outer_iter", profiled)
@@ -387,7 +403,7 @@ def main_dip(args, ctx):
                      "alg_bytes": alg_bytes,
                      "traffic_over_alg": (traffic / alg_bytes) if traffic and alg_bytes else None,
                      "flops_per_outer_iter": flops, "ms_per_outer_iter": dip_ms,
-                     "kernels": [ista_entry(f"k_ista_rs (lrs_ista_f32: {s.nb} blocks of {n} rows, Nit {nit}"
+                     "kernels": [ista_entry(ista_name
                                             + (f" over {n_sl:.0f} warm-started launches" if n_sl > 1 else "") + ")",
                                             ista_ms, ista_flops, f"{tag}_ista_hbm_bytes_per_launch", profiled)]},
         "mpsnr": {"input": mp0, "after_steps": mp1, "outer_iterations_run": args.warmup + args.steps},

@@ -128,6 +128,38 @@ int lrs_ista_f32(const float *Yb, const uint8_t *obs, const float *D, int64_t n,
                  int64_t K, int64_t nb, const float *alpha, const double *thr, int Nit, int prox,
                  float *coefs, float *phi, const lrs_ista_opts *opts, void *ws, size_t ws_bytes,
                  void *stream);
+/* ---- Masked ISTA on per-pattern Grams --------------------------------------------------------
+ * The same sparse coding as lrs_ista_f32 for blocks that share observation patterns.  ista()'s
+ * gradient H^T (y - H x) (main_LRS_PnP.py:131-149, …1-LiP.py:185-198, H = D pruned to the observed
+ * rows by delete_element :201-204) is expanded as b - Q_p x with Q_p = D^T diag(obs_pat[p]) D
+ * (fp64 sums of exact products, rounded to float32; formed once per call and pattern) and
+ * b = D^T (obs .* y) (once per block), so an inner iteration costs 2 K^2 instead of 4 n K FLOP per
+ * block.  Products on f32 matrix cores, the prox and the quotient as lrs_ista_f32: the results
+ * differ from it by rounding only.  K <= 512, any n (n_pad % 16 == 0), every prox; opts as
+ * lrs_ista_f32 (max_workgroups bounds the grid over tiles, warm_start continues from coefs;
+ * algorithm must be AUTO).
+ *   lrs_ista_pat_plan (host): groups the blocks by pattern.  pat: host int32 [nb], block j's row of
+ *     obs_pat (as lrs_ista_alpha_f32's patterns); plan: host int32 [cap >= lrs_ista_pat_plan_len]
+ *     = the blocks ordered by pattern (ascending within one), then per tile {first position,
+ *     pattern * 32 + count (1..16)}.  Returns the tile count (< 0: error).  Upload it as is.
+ *   lrs_ista_pat_preferred (host): 1 when this path does less matrix-core work than lrs_ista_f32's
+ *     row-split kernel for these sizes (few patterns, n > K / 2).
+ *   lrs_ista_pat_prepare: forms the dictionary images and every pattern's Q_p in ws
+ *     (lrs_ista_pat_workspace bytes), once per D and set of patterns (both fixed for a solve);
+ *     obs_pat DEVICE u8 [npat][n_pad].
+ *   lrs_ista_pat_f32: the sparse coding on the images ws holds (prepare first, again whenever D or
+ *     obs_pat change); plan DEVICE int32 (lrs_ista_pat_plan's); Yb [nb][n_pad], alpha/thr [nb] per
+ *     block. */
+int64_t lrs_ista_pat_plan_len(int64_t nb, int64_t npat);
+int64_t lrs_ista_pat_plan(const int32_t *pat, int64_t nb, int64_t npat, int32_t *plan, int64_t cap);
+int lrs_ista_pat_preferred(int64_t n, int64_t K, int64_t nb, int64_t npat, int Nit);
+size_t lrs_ista_pat_workspace(int64_t n, int64_t K, int64_t npat);
+int lrs_ista_pat_prepare(const float *D, int64_t n, int64_t K, const uint8_t *obs_pat, int64_t npat,
+                         int64_t n_pad, void *ws, size_t ws_bytes, void *stream);
+int lrs_ista_pat_f32(const float *Yb, const uint8_t *obs_pat, int64_t npat, const int32_t *plan,
+                     int64_t ntiles, int64_t n, int64_t n_pad, int64_t K, int64_t nb,
+                     const float *alpha, const double *thr, int Nit, int prox, float *coefs, float *phi,
+                     const lrs_ista_opts *opts, void *ws, size_t ws_bytes, void *stream);
 /* NLmeansfilter(g, 3, 3, h) (LRS-PnP(Matlab Code)/NLmeansfilter.m:18-78, the prox of
  * pnp_ista.m:30) of nvec columns of length K, fp64, 'symmetric' padding. */
 int lrs_nlm_matlab_col_f32(const float *g, int64_t ldg, float *out, int64_t ldo, int64_t K,

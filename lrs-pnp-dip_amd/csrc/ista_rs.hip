@@ -31,8 +31,7 @@
 
 #include <algorithm>
 
-#include "lrs_common.h"
-#include "lrs_nlm.h"
+#include "ista_prox.h"
 
 namespace lrs {
 
@@ -52,91 +51,11 @@ struct IstaRsParams {
     const float *x0;       // [nb][K] start coefficients (lrs_ista_opts.warm_start; may alias coefs) or null = 0
 };
 
-// numpy 'reflect' (no edge repeat) of index i into [0, K)
-__device__ __forceinline__ int reflect_idx(int i, int K) {
-    if (K == 1) return 0;
-    const int period = 2 * (K - 1);
-    i %= period;
-    if (i < 0) i += period;
-    return i >= K ? period - i : i;
-}
-
-// MATLAB 'symmetric' padding (edge repeated) of index i, |overhang| <= K
-__device__ __forceinline__ int symmetric_idx(int i, int K) {
-    if (i < 0) return -i - 1;
-    if (i >= K) return 2 * K - 1 - i;
-    return i;
-}
-
-// skimage 0.18.3 fast NLM of atoms a0..a0+3 of one gradient row in LDS
-__device__ __forceinline__ int gsw(int b, int a);
-
-__device__ __forceinline__ void prox_nlm_chunk(const float *row, int b, int a0, int K, double kneg, double c0,
-                                               double seven, float (&out)[4]) {
-    double w[11];
-#pragma unroll
-    for (int k = 0; k < 11; ++k) w[k] = (double)row[gsw(b, reflect_idx(a0 - 3 + k, K))];
-    int W1[7], W2[7], W3[7];
-    nlm_weights<true>(w, kneg, W1, W2, W3);
-    nlm_outputs<2>(w, W1, W2, W3, c0, seven, out);
-}
-
-// NLmeansfilter(g, 3, 3, h) of LRS-PnP(Matlab Code)/NLmeansfilter.m:18-78, one output, fp64, in the
-// evaluation order of oracle/nlm_oracle.c:oracle_nlm_matlab_col
-__device__ __forceinline__ float prox_nlm_matlab_point(const float *row, int b, int i, int K,
-                                                       const double (&krow)[7], double h2) {
-    double v[13];   // g-hat[i-6 .. i+6]
-#pragma unroll
-    for (int k = 0; k < 13; ++k) {
-        const int j = i - 6 + k;
-        v[k] = (j >= -3 && j < K + 3) ? (double)row[gsw(b, symmetric_idx(j, K))] : 0.0;
-    }
-    double sw = 0.0, av = 0.0, wmax = 0.0;
-#pragma unroll
-    for (int t = -3; t <= 3; ++t) {
-        const int r = i + t;
-        if (t == 0 || r < 0 || r >= K) continue;
-        double d = 0.0;
-#pragma unroll
-        for (int u = -3; u <= 3; ++u) {
-            const double df = v[6 + u] - v[6 + t + u];
-            d = d + krow[u + 3] * (df * df);
-        }
-        const double wt = exp(-d / h2);
-        if (wt > wmax) wmax = wt;
-        sw = sw + wt;
-        av = av + wt * v[6 + t];
-    }
-    av = av + wmax * v[6];
-    sw = sw + wmax;
-    return sw > 0.0 ? (float)(av / sw) : row[gsw(b, i)];
-}
-
-__device__ __forceinline__ void nlm_matlab_krow_d(double (&krow)[7]) {
-#pragma unroll
-    for (int u = -3; u <= 3; ++u) {
-        const int a = u < 0 ? -u : u;
-        double s = 0.0;
-        for (int d = (a < 1 ? 1 : a); d <= 3; ++d) s = s + 1.0 / (double)(2 * d + 1);
-        krow[u + 3] = s / 3.0;
-    }
-}
-
-// a / b from y = 1/b (correctly rounded reciprocal) and one remainder step: the IEEE quotient
-// away from overflow / underflow (…1-LiP.py:190 torch division by alpha)
-__device__ __forceinline__ float rs_div(float a, float b, float y) {
-    const float q = a * y;
-    const float r = __fmaf_rn(-b, q, a);
-    return __fmaf_rn(r, y, q);
-}
-
 // LDS of one workgroup (floatx4 = 16 B units of [tile][lane]):
 //   part  [NQ atom tiles][S-1 partial G images][64]     (S = 1: none)
 //   xbuf  [NQ][64]            the coefficients x: B operand of every R_t, rewritten by the prox
 //   gbuf  [16 blocks][NQ*16]  the gradient rows read by the prox (chunk index XOR-swizzled by block)
 __host__ __device__ constexpr size_t rs_lds_bytes(int NQ, int S) { return (size_t)(S + 1) * NQ * 1024; }
-
-__device__ __forceinline__ int gsw(int b, int a) { return a ^ ((b & 15) << 2); }
 
 // The observation term is split off the residual: D^T (m .* (y - D x)) = b - D^T (m .* D x) with
 // b = D^T (m .* y) formed once per launch (each owner keeps its atom tiles of b in VGPRs), so the
@@ -498,6 +417,15 @@ static int launch_rs(const IstaRsParams &p, int NT, int64_t max_wg, hipStream_t 
     case 3: return launch_rs_k<NQ, MINW, 3>(p, max_wg, st);
     default: return launch_rs_k<NQ, MINW, 4>(p, max_wg, st);
     }
+}
+
+// the two fragment-ordered dictionary images (also used by the per-pattern Gram kernel, ista_pat.hip)
+int ista_rs_images(const float *D, int64_t n, int64_t K, int NT, int NQ, float4 *DAf, float4 *DTf, hipStream_t st) {
+    const int64_t total = (int64_t)NT * NQ * 64;
+    const unsigned blocks = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(k_ista_rs_prep, dim3(blocks), dim3(256), 0, st, D, (int)n, (int)K, NT, NQ, DAf, DTf);
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
 }
 
 int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t n, int64_t n_pad, int64_t K, int64_t nb,

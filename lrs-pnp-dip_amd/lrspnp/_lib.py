@@ -83,6 +83,13 @@ def _declare(L):
         "lrs_ista_f32": (i32, [vp, vp, vp, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp, c.POINTER(IstaOpts), vp,
                                sz, vp]),
         "lrs_nlm_matlab_col_f32": (i32, [vp, i64, vp, i64, i64, i64, f64, vp, vp]),
+        "lrs_ista_pat_plan_len": (i64, [i64, i64]),
+        "lrs_ista_pat_plan": (i64, [i32p, i64, i64, i32p, i64]),
+        "lrs_ista_pat_preferred": (i32, [i64, i64, i64, i64, i32]),
+        "lrs_ista_pat_workspace": (sz, [i64, i64, i64]),
+        "lrs_ista_pat_prepare": (i32, [vp, i64, i64, vp, i64, i64, vp, sz, vp]),
+        "lrs_ista_pat_f32": (i32, [vp, vp, i64, vp, i64, i64, i64, i64, i64, vp, vp, i32, i32, vp, vp,
+                                   c.POINTER(IstaOpts), vp, sz, vp]),
         "lrs_ssim_f32": (i32, [vp, vp, i32, i32, i32, vp, vp]),
         "lrs_psnr_workspace": (sz, [i64, i64]),
         "lrs_psnr_bands_f32": (i32, [vp, vp, i64, i64, vp, vp, sz, vp]),

@@ -15,7 +15,7 @@ from ._lib import (ALPHA_FRO4, ALPHA_SOFT, ALPHA_SPEC2, PROX_NLM, PROX_NLM_MATLA
                    device_lib, lib)
 
 __all__ = ["nlm_col", "block_grid", "cover_ranges", "im2col", "ista_alpha", "ista", "svt_workspace",
-           "ista_workspace", "nlm_matlab_col", "svt", "svt_gram", "svt_gram_view", "svt_finish", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT",
+           "ista_workspace", "ista_pat_plan", "ista_pat_preferred", "ista_pat_workspace", "ista_pat_prepare", "ista_pat", "nlm_matlab_col", "svt", "svt_gram", "svt_gram_view", "svt_finish", "admm_update", "unfolded_to_image", "image_to_unfolded", "ALPHA_SPEC2", "ALPHA_FRO4", "ALPHA_SOFT", "PROX_NLM", "PROX_SOFT",
            "PROX_NLM_MATLAB"]
 
 
@@ -160,6 +160,80 @@ def ista(Yb, obs, D, n: int, alpha, thr, Nit: int, prox: int = PROX_NLM, phi=Non
     check(L.lrs_ista_f32(_p(Yb), _p(obs), _p(D), n, n_pad, K, nb, _p(alpha), _p(thr), int(Nit), int(prox),
                          _p(coefs) if want_coefs else None, _p(phi), opts, _p(ws), 0 if ws is None else ws.numel(),
                          _s(stream)), "lrs_ista_f32")
+    return (phi, coefs) if want_coefs else phi
+
+
+def ista_pat_plan(pat, npat: int):
+    """Blocks grouped by observation pattern (lrs_ista_pat_plan, host): returns (plan int32 numpy
+    array, ntiles).  pat: block j's pattern index in [0, npat) (host int32 array)."""
+    L = lib()
+    pat = np.ascontiguousarray(np.asarray(pat), dtype=np.int32)
+    nb = pat.size
+    cap = int(L.lrs_ista_pat_plan_len(nb, int(npat)))
+    if cap < 0:
+        check(cap, "lrs_ista_pat_plan_len")
+    plan = np.zeros(cap, np.int32)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    nt = int(L.lrs_ista_pat_plan(pat.ctypes.data_as(i32p), nb, int(npat), plan.ctypes.data_as(i32p), cap))
+    if nt < 0:
+        check(nt, "lrs_ista_pat_plan")
+    return plan, nt
+
+
+def ista_pat_preferred(n: int, K: int, nb: int, npat: int, Nit: int) -> bool:
+    """Whether the per-pattern Gram path does less matrix-core work than the row-split kernel."""
+    return bool(lib().lrs_ista_pat_preferred(int(n), int(K), int(nb), int(npat), int(Nit)))
+
+
+def ista_pat_workspace(n: int, K: int, npat: int, device) -> torch.Tensor:
+    return torch.empty(max(int(lib().lrs_ista_pat_workspace(int(n), int(K), int(npat))), 1), dtype=torch.uint8,
+                       device=device)
+
+
+def ista_pat_prepare(D, obs_pat, n: int, ws=None, stream=None) -> torch.Tensor:
+    """The dictionary images and every pattern's masked Gram Q_p = D^T diag(m_p) D in `ws`
+    (lrs_ista_pat_prepare; allocated here when None); returns ws, which ista_pat() then reads."""
+    L = device_lib()
+    _dev(D, torch.float32, "D")
+    _dev(obs_pat, torch.uint8, "obs_pat")
+    K = D.shape[1]
+    npat, n_pad = obs_pat.shape
+    if ws is None:
+        ws = ista_pat_workspace(n, K, npat, D.device)
+    check(L.lrs_ista_pat_prepare(_p(D), n, K, _p(obs_pat), npat, n_pad, _p(ws), ws.numel(), _s(stream)),
+          "lrs_ista_pat_prepare")
+    return ws
+
+
+def ista_pat(Yb, obs_pat, plan, ntiles: int, K: int, n: int, alpha, thr, Nit: int, ws, prox: int = PROX_NLM,
+             phi=None, coefs=None, want_coefs=False, stream=None, max_workgroups: int = 0, warm_start: bool = False):
+    """Masked ISTA + prox on per-pattern Grams (lrs_ista_pat_f32) for blocks that share observation
+    patterns, on the images ista_pat_prepare() left in `ws`.  obs_pat (npat, n_pad) u8 and plan
+    (ista_pat_plan's, as an int32 device tensor) on the device; the rest as ista().  Returns
+    phi [, coefs]."""
+    L = device_lib()
+    _dev(Yb, torch.float32, "Yb")
+    _dev(obs_pat, torch.uint8, "obs_pat")
+    _dev(plan, torch.int32, "plan")
+    _dev(alpha, torch.float32, "alpha")
+    _dev(thr, torch.float64, "thr")
+    _dev(ws, torch.uint8, "ws")
+    nb, n_pad = Yb.shape
+    npat = obs_pat.shape[0]
+    if phi is None:
+        phi = torch.empty((nb, n_pad), dtype=torch.float32, device=Yb.device)
+    if warm_start:
+        if coefs is None:
+            raise LrsError("ista_pat(warm_start=True) continues from `coefs`: pass it")
+        want_coefs = True
+    if want_coefs and coefs is None:
+        coefs = torch.empty((nb, K), dtype=torch.float32, device=Yb.device)
+    opts = None
+    if max_workgroups or warm_start:
+        opts = ctypes.byref(_libmod.ista_opts(_libmod.ISTA_SPLIT_BF16, int(max_workgroups), 0, 1 if warm_start else 0))
+    check(L.lrs_ista_pat_f32(_p(Yb), _p(obs_pat), npat, _p(plan), int(ntiles), n, n_pad, int(K), nb, _p(alpha),
+                             _p(thr), int(Nit), int(prox), _p(coefs) if want_coefs else None, _p(phi), opts, _p(ws),
+                             ws.numel(), _s(stream)), "lrs_ista_pat_f32")
     return (phi, coefs) if want_coefs else phi
 
 

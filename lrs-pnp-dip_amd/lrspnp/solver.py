@@ -55,6 +55,14 @@ class LrsPnPConfig:
     # place the DIP's workgroups first.  Measured at configs[2] (bench.py --lowrank-priority, 2
     # alternating rounds): 0 -> 7.43 / 7.43 outer it/s, -1 -> 7.48 / 7.41: no effect, so 0.
     lowrank_priority: int = 0
+    # Order of the sparse coding and the DIP training (lowrank='dip'): "beside" runs the
+    # sparse-coding kernel concurrently with the DIP's first steps; "before" makes the DIP's stream
+    # wait for it (the kernel then has the chip to itself).
+    ista_dip_order: str = "beside"
+    # Sparse coding on per-pattern masked Grams (lrs_ista_pat_f32: the blocks grouped by observation
+    # pattern, 2 K^2 instead of 4 n K FLOP per block and iteration): "auto" when the library's cost
+    # model prefers it (few patterns, n > K / 2), "on" whenever the block length allows it, "off".
+    ista_patterns: str = "auto"
 
     @staticmethod
     def dip_1lip(**kw) -> "LrsPnPConfig":
@@ -144,6 +152,13 @@ class LrsPnP:
         self.alpha = alpha_pat.index_select(0, inv_d).contiguous()
         self.thr = thr_pat.index_select(0, inv_d).contiguous()
         self.alpha_pat, self.thr_pat, self.obs_pat = alpha_pat, thr_pat, obs_pat
+        self.pat_plan = None
+        if cfg.ista_patterns not in ("auto", "on", "off"):
+            raise LrsError(f"unknown ista_patterns {cfg.ista_patterns!r} (auto | on | off)")
+        if self.K <= 512 and (cfg.ista_patterns == "on" or (
+                cfg.ista_patterns == "auto" and ops.ista_pat_preferred(n, self.K, self.nb, self.npat, cfg.Nit))):
+            plan, self.pat_ntiles = ops.ista_pat_plan(inv.reshape(-1), self.npat)
+            self.pat_plan = t(plan)
 
         # ---- state and buffers -------------------------------------------------------------
         self.X = self.Y.clone()                           # X = Y_observed     main_LRS_PnP.py:229
@@ -152,7 +167,10 @@ class LrsPnP:
         self.U = torch.empty_like(self.Y)
         self.Yb = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
         self.phi = torch.empty((self.nb, self.n_pad), dtype=torch.float32, device=dev)
-        self.ista_ws = ops.ista_workspace(n, self.K, self.prox, dev)
+        if self.pat_plan is not None:   # the dictionary and Gram images, once per solve (D, patterns fixed)
+            self.ista_ws = ops.ista_pat_prepare(self.D, self.obs_pat, n)
+        else:
+            self.ista_ws = ops.ista_workspace(n, self.K, self.prox, dev)
         self.norms = torch.zeros(3, dtype=torch.float64, device=dev)
         self.lowrank_stream = torch.cuda.Stream(device=dev, priority=int(cfg.lowrank_priority))
         self.iteration = 0
@@ -191,8 +209,18 @@ class LrsPnP:
         """Yb = blocks of X + L1/mu1; Phi = D * ISTA-PnP(Yb) for every block."""
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
                    stream=stream)
-        return ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox,
-                        phi=self.phi, want_coefs=want_coefs, ws=self.ista_ws, stream=stream)
+        return self._ista(self.cfg.Nit, stream, want_coefs=want_coefs)
+
+    def _ista(self, Nit, stream, want_coefs=False, coefs=None, warm_start=False, max_workgroups=0):
+        """All blocks' ISTA into self.phi: the per-pattern Gram path when planned, else lrs_ista_f32."""
+        if self.pat_plan is not None:
+            return ops.ista_pat(self.Yb, self.obs_pat, self.pat_plan, self.pat_ntiles, self.K, self.n, self.alpha,
+                                self.thr, Nit, self.ista_ws, self.prox, phi=self.phi, coefs=coefs,
+                                want_coefs=want_coefs, stream=stream, max_workgroups=max_workgroups,
+                                warm_start=warm_start)
+        return ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, Nit, self.prox, phi=self.phi,
+                        coefs=coefs, want_coefs=want_coefs, ws=self.ista_ws, stream=stream,
+                        max_workgroups=max_workgroups, warm_start=warm_start)
 
     def sparse_coding_range(self, b0: int, b1: int, stream=None):
         """Phi rows [b0, b1) only (the blocks of one task-parallel worker, lrspnp.dist.DipTaskSplit)."""
@@ -200,8 +228,9 @@ class LrsPnP:
             return
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d[b0:b1], self.cols_d[b0:b1], self.n_pad,
                    Yb=self.Yb[b0:b1], stream=stream)
+        ws = self.ista_ws if self.pat_plan is None else None   # a block range runs the row-split kernel
         ops.ista(self.Yb[b0:b1], self.obs[b0:b1], self.D, self.n, self.alpha[b0:b1], self.thr[b0:b1], self.cfg.Nit,
-                 self.prox, phi=self.phi[b0:b1], ws=self.ista_ws, stream=stream)
+                 self.prox, phi=self.phi[b0:b1], ws=ws, stream=stream)
 
     def admm(self, stream=None):
         """col2im + closed-form X + dual updates from the current Phi and U (main_LRS_PnP.py:324-366)."""
@@ -250,8 +279,7 @@ class LrsPnP:
             # solve starts at once; the tridiagonal chain fits inside the sparse coding even when
             # its Gram waits for the first sparse-coding workgroups to retire
             main.wait_event(gram_done)
-        ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
-                 ws=self.ista_ws, stream=main)
+        self._ista(self.cfg.Nit, main)
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
                         self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)
@@ -267,18 +295,20 @@ class LrsPnP:
         rs = self.n_pad > 64 and self.D.shape[1] <= 512   # the row-split kernel (warm start) serves
         sl = max(1, min(int(self.cfg.ista_slices_dip), self.cfg.Nit)) if rs else 1
         if sl == 1:
-            ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, self.cfg.Nit, self.prox, phi=self.phi,
-                     ws=self.ista_ws, stream=main, max_workgroups=self.cfg.ista_max_wg_dip)
+            self._ista(self.cfg.Nit, main, max_workgroups=self.cfg.ista_max_wg_dip)
         else:   # time-sliced: Nit split over `sl` launches continuing from the coefficients
             if getattr(self, "_coefs", None) is None:
                 self._coefs = torch.empty((self.nb, self.D.shape[1]), dtype=torch.float32, device=self.Yb.device)
             done = 0
             for k in range(sl):
                 it = (self.cfg.Nit * (k + 1)) // sl - done
-                ops.ista(self.Yb, self.obs, self.D, self.n, self.alpha, self.thr, it, self.prox, phi=self.phi,
-                         coefs=self._coefs, want_coefs=True, warm_start=k > 0, ws=self.ista_ws, stream=main,
-                         max_workgroups=self.cfg.ista_max_wg_dip)
+                self._ista(it, main, coefs=self._coefs, want_coefs=True, warm_start=k > 0,
+                           max_workgroups=self.cfg.ista_max_wg_dip)
                 done += it
+        if self.cfg.ista_dip_order == "before":
+            lr.wait_stream(main)
+        elif self.cfg.ista_dip_order != "beside":
+            raise LrsError(f"unknown ista_dip_order {self.cfg.ista_dip_order!r} (beside | before)")
         self.low_rank_dip(lr)
         main.wait_stream(lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,

@@ -72,3 +72,43 @@ def test_invalid_arguments_rejected():
     assert L.lrs_ista_f32(None, None, None, 64, 64, 256, 10, None, None, 10, 0, None, None, None, None, 0,
                           None) == -1
     assert L.lrs_nlm_col_f32(None, 0, None, 0, 0, 0, 0.0, None, 3, 3, None) == -1
+
+
+def test_ista_pattern_plan():
+    """lrs_ista_pat_plan (host): the blocks grouped by observation pattern, ascending within one,
+    in tiles of at most 16 blocks of a single pattern; malformed pattern indices refused."""
+    from lrspnp import ops
+    rng = np.random.default_rng(5)
+    for nb, npat in [(1, 1), (16, 1), (17, 1), (100, 7), (6408, 27), (513, 300)]:
+        pat = rng.integers(0, npat, nb).astype(np.int32)
+        plan, nt = ops.ista_pat_plan(pat, npat)
+        order, tiles = plan[:nb], plan[nb:nb + 2 * nt].reshape(nt, 2)
+        assert sorted(order.tolist()) == list(range(nb))
+        seen = []
+        for start, pc in tiles:
+            p, c = pc >> 5, pc & 31
+            assert 1 <= c <= 16
+            blk = order[start:start + c]
+            assert np.all(pat[blk] == p) and np.all(np.diff(blk) > 0)
+            seen.extend(blk.tolist())
+        assert sorted(seen) == list(range(nb))
+        counts = np.bincount(pat, minlength=npat)
+        assert nt == int(np.sum((counts + 15) // 16))
+    L = _lib.lib()
+    bad = np.array([0, 3], np.int32)
+    out = np.zeros(64, np.int32)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    assert L.lrs_ista_pat_plan(bad.ctypes.data_as(i32p), 2, 3, out.ctypes.data_as(i32p), 64) < 0
+    assert L.lrs_ista_pat_plan(bad.ctypes.data_as(i32p), 2, 4, out.ctypes.data_as(i32p), 1) < 0
+
+
+def test_ista_pattern_cost_model():
+    """The per-pattern Gram path is chosen for the DIP mains' blocks (n = 1296, K = 256, 27 patterns
+    for 6,408 blocks on the bench cube) and not when every block has its own pattern, nor for
+    bb = 8 blocks (n = 64 < K / 2)."""
+    from lrspnp import ops
+    assert ops.ista_pat_preferred(1296, 256, 6408, 27, 100)
+    assert ops.ista_pat_preferred(1296, 256, 50974, 24, 100)
+    assert not ops.ista_pat_preferred(1296, 256, 6408, 6408, 100)
+    assert not ops.ista_pat_preferred(64, 256, 125000, 40, 80)
+    assert not ops.ista_pat_preferred(1296, 768, 6408, 27, 100)   # K > 512: the generic path

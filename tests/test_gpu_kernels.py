@@ -131,6 +131,93 @@ def test_ista_kernel_vs_oracle(ops, bb, nb, Nit, variant, K):
     assert worst_phi < tol, (worst_phi, tol)
 
 
+def _pattern_blocks(rng, nb, n, npat, miss_frac, scale=0.3):
+    """Blocks that share `npat` observation patterns (ragged: one pattern holds > 16 blocks, one a
+    single block); returns Yb, obs (per block), obs_pat, pat."""
+    pats = (rng.random((npat, n)) > miss_frac).astype(np.uint8)
+    pats[0, :] = 1
+    if npat > 1:
+        pats[1, : n // 2] = 0
+    pat = rng.integers(0, npat, nb).astype(np.int32)
+    pat[: min(nb, 18)] = 0
+    if npat > 2:
+        pat[pat == 2] = 3 % npat
+        pat[-1] = 2
+    obs = pats[pat]
+    Yb = (rng.standard_normal((nb, n)) * scale).astype(np.float32)
+    Yb[obs == 0] = 0.0
+    return Yb, obs, pats, pat
+
+
+def _pattern_case(ops, bb, nb, Nit, variant, K, npat, seed):
+    from lrspnp.data import synthetic_dictionary
+    rng = np.random.default_rng(seed)
+    n = bb * bb
+    n_pad = -(-n // 16) * 16
+    D = synthetic_dictionary(n, K, seed=3)
+    Yb, obs, pats, pat = _pattern_blocks(rng, nb, n, npat, 0.2)
+    ap = np.empty(npat, np.float32); tp = np.empty(npat, np.float64)
+    for k in range(npat):
+        ap[k], tp[k] = O.ista_alpha_h(D[pats[k].astype(bool)], 0.1, variant)
+    alpha, thr = ap[pat], tp[pat]
+    prox = {"soft": O.PROX_SOFT, "matlab": O.PROX_NLM_MATLAB}.get(variant, O.PROX_NLM)
+    pad = lambda a: np.pad(a, ((0, 0), (0, n_pad - n)))
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    plan, nt = ops.ista_pat_plan(pat, npat)
+    ws = ops.ista_pat_prepare(d(D), d(pad(pats)), n)
+    args = dict(Yb=d(pad(Yb)), obs_pat=d(pad(pats)), plan=d(plan), ntiles=nt, K=K, n=n, alpha=d(alpha),
+                thr=d(thr), Nit=Nit, ws=ws, prox=prox)
+    return rng, n, D, Yb, obs, alpha, thr, prox, args, d, pad
+
+
+@pytest.mark.parametrize("bb,nb,Nit,variant,K,npat", [
+    (36, 40, 12, "fro4", 256, 3), (36, 37, 10, "spec2", 256, 5), (36, 21, 8, "soft", 256, 2),
+    (36, 19, 6, "matlab", 256, 4), (36, 35, 10, "fro4", 128, 3), (36, 18, 8, "fro4", 512, 2),
+    (36, 23, 10, "fro4", 200, 4), (20, 50, 10, "fro4", 256, 6), (8, 40, 10, "fro4", 7, 3),
+    (8, 33, 12, "spec2", 64, 2), (36, 3, 100, "fro4", 256, 1), (36, 70, 1, "fro4", 256, 3)])
+def test_ista_pattern_gram_vs_oracle(ops, bb, nb, Nit, variant, K, npat):
+    """The per-pattern Gram path (lrs_ista_pat_f32: g = x + (b - Q_p x) / alpha) against the oracle's
+    per-block ista() at 1e-5 (the MATLAB prox: its own sensitivity bar, as above), and against the
+    row-split kernel on the same blocks at 1e-5."""
+    rng, n, D, Yb, obs, alpha, thr, prox, args, d, pad = _pattern_case(ops, bb, nb, Nit, variant, K, npat,
+                                                                        bb * 7 + nb + K + npat)
+    Xo, PHIo = O.ista_batch(Yb, obs, D, alpha, thr, Nit, prox)
+    phi, coefs = ops.ista_pat(**args, want_coefs=True)
+    assert np.all(phi.cpu().numpy()[:, n:] == 0)
+    phi = phi.cpu().numpy()[:, :n]
+    coefs = coefs.cpu().numpy()
+    tol = 1e-5
+    if variant == "matlab" and Nit > 1:
+        flip = np.where(rng.random(Yb.shape) < 0.5, -1.0, 1.0)
+        Yp = (Yb.astype(np.float64) * (1.0 + flip * 2.0 ** -23)).astype(np.float32)
+        Xp, PHIp = O.ista_batch(Yp, obs, D, alpha, thr, Nit, prox)
+        sens = max(max(rel(Xp[j], Xo[j]) for j in range(nb)), max(rel(PHIp[j], PHIo[j]) for j in range(nb)))
+        tol = max(1e-5, 4.0 * sens)
+    assert max(rel(coefs[j], Xo[j]) for j in range(nb)) < tol
+    assert max(rel(phi[j], PHIo[j]) for j in range(nb)) < tol
+    phr, cor = ops.ista(args["Yb"], d(pad(obs)), d(D), n, args["alpha"], args["thr"], Nit, prox, want_coefs=True)
+    assert max(rel(coefs[j], cor.cpu().numpy()[j]) for j in range(nb)) < max(tol, 1e-5)
+
+
+def test_ista_pattern_gram_grid_and_warm_start_bitwise(ops):
+    """lrs_ista_pat_f32's bounded grid (max_workgroups) and warm-start slices give the one-launch
+    result bit for bit; repeated calls are deterministic."""
+    _, n, D, Yb, obs, alpha, thr, prox, args, d, pad = _pattern_case(ops, 36, 16 * 5 + 7, 12, "fro4", 256, 4, 91)
+    phi0, c0 = ops.ista_pat(**args, want_coefs=True)
+    phi1, c1 = ops.ista_pat(**args, want_coefs=True, max_workgroups=2)
+    assert torch.equal(phi0, phi1) and torch.equal(c0, c1)
+    phi2, c2 = ops.ista_pat(**args, want_coefs=True)
+    assert torch.equal(phi0, phi2) and torch.equal(c0, c2)
+    a = dict(args)
+    co = torch.zeros_like(c0)
+    done = 0
+    for k, it in enumerate((5, 4, 3)):
+        a["Nit"] = it
+        ph, _ = ops.ista_pat(**a, coefs=co, want_coefs=True, warm_start=k > 0)
+        done += it
+    assert done == 12 and torch.equal(co, c0) and torch.equal(ph, phi0)
+
+
 @pytest.mark.parametrize("bb,nb,Nit,variant,K", [(36, 23, 10, "fro4", 256), (8, 70, 20, "spec2", 256),
                                                   (36, 12, 6, "soft", 100), (20, 19, 9, "fro4", 512)])
 def test_ista_generic_path_vs_oracle(ops, bb, nb, Nit, variant, K):

@@ -181,15 +181,18 @@ def test_config1_two_outer_iterations_vs_oracle_fixture(gpu, golden):
         assert np.allclose(s.convergence(), g["norms"][it], rtol=1e-4)
 
 
-def test_config2_sparse_coding_vs_oracle_fixture(gpu, golden):
+@pytest.mark.parametrize("patterns", ["auto", "off"])
+def test_config2_sparse_coding_vs_oracle_fixture(gpu, golden, patterns):
     """BASELINE configs[2]'s sparse coding at full size (196x196x198, bb 36, 6,408 blocks, fro4,
-    Nit 100): the row-split ISTA kernel's Phi and coefficients of every 53rd block of the first
-    outer iteration against the oracle C ISTA at 1e-5 relative L2 (per block and overall)."""
+    Nit 100): Phi and coefficients of every 53rd block of the first outer iteration against the
+    oracle C ISTA at 1e-5 relative L2 (per block and overall), on the per-pattern Gram path the
+    solver picks for this cube (27 observation patterns) and on the row-split kernel."""
     from lrspnp import LrsPnP, LrsPnPConfig
     g = golden("cube196_bb36_sc.npz")
     Y, M, D, _ = _bench_problem(196, 196, 198, 36)
-    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_1lip(lowrank="svt"))
+    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_1lip(lowrank="svt", ista_patterns=patterns))
     assert s.nb == 6408
+    assert (s.pat_plan is not None) == (patterns == "auto") and s.npat < 64
     phi, coefs = s.sparse_coding(want_coefs=True)
     torch.cuda.synchronize()
     sel = torch.from_numpy(g["blocks"]).cuda()
@@ -200,14 +203,17 @@ def test_config2_sparse_coding_vs_oracle_fixture(gpu, golden):
         assert rel(ph[k], g["phi"][k]) < 1e-5, k
 
 
-def test_config3_sparse_coding_vs_oracle_fixture(gpu, golden):
+@pytest.mark.parametrize("patterns", ["auto", "off"])
+def test_config3_sparse_coding_vs_oracle_fixture(gpu, golden, patterns):
     """BASELINE configs[3]'s sparse coding at full size (512x512x224, bb 36, 50,974 blocks, fro4,
-    Nit 100; main_LRS_PnP_DIP_pro.py:375-400): the row-split ISTA kernel's coefficients of every 53rd
-    block and Phi of every 212th against the oracle C ISTA at 1e-5 relative L2."""
+    Nit 100; main_LRS_PnP_DIP_pro.py:375-400): coefficients of every 53rd block and Phi of every
+    212th against the oracle C ISTA at 1e-5 relative L2, per-pattern Gram path (24 patterns) and
+    row-split kernel."""
     from lrspnp import LrsPnP, LrsPnPConfig
     g = golden("cube512_bb36_sc.npz")
     Y, M, D, _ = _bench_problem(512, 512, 224, 36)
-    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_pro(lowrank="svt"))
+    s = LrsPnP(Y, M, D, LrsPnPConfig.dip_pro(lowrank="svt", ista_patterns=patterns))
+    assert (s.pat_plan is not None) == (patterns == "auto")
     assert s.nb == int(g["nb"]) == 50974
     phi, coefs = s.sparse_coding(want_coefs=True)
     torch.cuda.synchronize()

@@ -21,12 +21,12 @@ from lrspnp import LrsPnP, LrsPnPConfig, _lib  # noqa: E402
 from lrspnp.data import load_fixture, mask_matrix, synthetic_cube, synthetic_dictionary, unfold  # noqa: E402
 
 
-def run(name, H, W, B, bb, nit, variant, reps, K=256):
+def run(name, H, W, B, bb, nit, variant, reps, K=256, patterns="auto"):
     base = load_fixture("data_img5.npz")["lrs_mask"]
     obs, clean, mask = synthetic_cube(H, W, B, seed=0, base_mask=base)
     Y, M = unfold(obs), mask_matrix(mask, B)
     D = synthetic_dictionary(bb * bb, K, 0)
-    s = LrsPnP(Y, M, D, LrsPnPConfig(bb=bb, sliding=bb, Nit=nit, variant=variant))
+    s = LrsPnP(Y, M, D, LrsPnPConfig(bb=bb, sliding=bb, Nit=nit, variant=variant, ista_patterns=patterns))
     st = torch.cuda.current_stream()
     s.sparse_coding(stream=st)
     torch.cuda.synchronize()
@@ -39,9 +39,11 @@ def run(name, H, W, B, bb, nit, variant, reps, K=256):
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     n = bb * bb
-    flops = nit * s.nb * 4 * n * K + s.nb * 2 * n * K
+    pat = s.pat_plan is not None
+    flops = (s.nb * (4 * n * K + nit * 2 * K * K) if pat else nit * s.nb * 4 * n * K + s.nb * 2 * n * K)
     ms = float(np.median(ts))
-    print(json.dumps({"workload": name, "blocks": s.nb, "ms": ms, "ms_all": ts, "gflop": flops / 1e9,
+    print(json.dumps({"workload": name, "blocks": s.nb, "path": "pattern-gram" if pat else "row-split",
+                      "npat": s.npat, "ms": ms, "ms_all": ts, "gflop": flops / 1e9,
                       "tflops": flops / ms / 1e9, "frac_f32_peak": flops / ms / 1e9 / 157.3}), flush=True)
 
 
@@ -49,6 +51,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--patterns", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--variant", default=None, help="override the ISTA variant (e.g. soft: prox ablation)")
     a = ap.parse_args()
     jobs = [("cfg2_196x196x198_bb36_fro4", 196, 196, 198, 36, 100, "fro4"),
             ("native_36x36x128_bb36_fro4", 36, 36, 128, 36, 100, "fro4"),
@@ -57,7 +61,10 @@ def main():
     for j in jobs:
         if a.only and a.only not in j[0]:
             continue
-        run(*j, reps=a.reps)
+        j = list(j)
+        if a.variant:
+            j[6] = a.variant
+        run(*j, reps=a.reps, patterns=a.patterns)
 
 
 if __name__ == "__main__":
