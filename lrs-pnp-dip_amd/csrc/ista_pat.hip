@@ -155,8 +155,16 @@ __global__ __launch_bounds__(64 * S) void k_ista_pat(IstaPatParams p) {
         return acc;
     };
 
-    for (int64_t tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
-        if (tile != blockIdx.x) __syncthreads();   // the previous tile's last reads of xbuf / gbuf are done
+    // XCD-aware tile order: workgroup b runs on XCD b % 8 (round-robin dispatch), so with one
+    // workgroup per tile XCD x takes the x-th contiguous eighth of the (pattern-major) tile list and
+    // its L2 holds only those patterns' Q images (all 27 of the bench cube: 6.9 MB > 4 MB per XCD)
+    int64_t first = blockIdx.x;
+    if (gridDim.x == p.ntiles) {
+        const int64_t q = p.ntiles >> 3, r = p.ntiles & 7, x = blockIdx.x & 7, i = blockIdx.x >> 3;
+        first = x * q + std::min<int64_t>(x, r) + i;
+    }
+    for (int64_t tile = first; tile < p.ntiles; tile += gridDim.x) {
+        if (tile != first) __syncthreads();   // the previous tile's last reads of xbuf / gbuf are done
         // tile descriptor (clamped: a malformed plan cannot address outside the arrays)
         const int64_t start = tiles[2 * tile];
         const int pc = tiles[2 * tile + 1];
@@ -270,7 +278,7 @@ __global__ __launch_bounds__(64 * S) void k_ista_pat(IstaPatParams p) {
                     for (int e = 0; e < 4; ++e)
                         o[e] = a0 + e < K ? prox_nlm_matlab_point(row, jl, a0 + e, K, krow, h2) : 0.f;
                 } else {
-                    prox_nlm_chunk(row, jl, a0, K, nlm_kneg(th), c0, p.seven, o);
+                    prox_nlm_chunk_v4(row, jl, a0, K, nlm_kneg(th), c0, p.seven, o);
                 }
                 xbuf[q * 64 + lane] = floatx4{a0 < K ? o[0] : 0.f, a0 + 1 < K ? o[1] : 0.f, a0 + 2 < K ? o[2] : 0.f,
                                               a0 + 3 < K ? o[3] : 0.f};

@@ -27,6 +27,28 @@ __device__ __forceinline__ int symmetric_idx(int i, int K) {
 // gradient-row chunk index XOR-swizzled by block: [16 blocks][KP] floats read by the prox
 __device__ __forceinline__ int gsw(int b, int a) { return a ^ ((b & 15) << 2); }
 
+// The same chunk with the interior window (a0 - 3 .. a0 + 7 inside [0, K)) read as three aligned
+// 16-byte LDS loads (the swizzle keeps 4-float groups contiguous); identical values and outputs.
+__device__ __forceinline__ void prox_nlm_chunk_v4(const float *row, int b, int a0, int K, double kneg, double c0,
+                                                  double seven, float (&out)[4]) {
+    double w[11];
+    if (a0 >= 4 && a0 + 8 <= K) {
+        float4 v[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) v[u] = *reinterpret_cast<const float4 *>(&row[gsw(b, a0 - 4 + 4 * u)]);
+        const float f[12] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                             v[2].x, v[2].y, v[2].z, v[2].w};
+#pragma unroll
+        for (int k = 0; k < 11; ++k) w[k] = (double)f[k + 1];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 11; ++k) w[k] = (double)row[gsw(b, reflect_idx(a0 - 3 + k, K))];
+    }
+    int W1[7], W2[7], W3[7];
+    nlm_weights<true>(w, kneg, W1, W2, W3);
+    nlm_outputs<2>(w, W1, W2, W3, c0, seven, out);
+}
+
 __device__ __forceinline__ void prox_nlm_chunk(const float *row, int b, int a0, int K, double kneg, double c0,
                                                double seven, float (&out)[4]) {
     double w[11];
