@@ -190,10 +190,16 @@ typedef struct {
  *     Davis-Kahan orthogonality certificate, falling back (inside the same workgroup) to the
  *     Jacobi solve when the certificate fails (clustered / repeated eigenvalues);
  *   LRS_SVT_JACOBI: the cyclic Jacobi solver only, warm-started from the previous call's
- *     eigenvectors kept in ws when LRS_SVT_WARM is also set.
- * s_out (nullable, device, B doubles) receives the singular values (descending). */
+ *     eigenvectors kept in ws when LRS_SVT_WARM is also set;
+ *   LRS_SVT_MULTI_WG (default path only): the same solver with its eigenvalue, inverse-iteration
+ *     and back-transformation phases spread over many workgroups (bit-identical result); for a
+ *     caller whose eigensolver is on the critical path (a row-slab shard), not beside a
+ *     chip-filling sparse-coding kernel.
+ * s_out (nullable, device, B doubles) receives the singular values (descending).  B <= 198 (the
+ * eigensolver holds the packed fp64 Gram in one CU's LDS); LRS_E_UNSUPPORTED above. */
 #define LRS_SVT_WARM 1
 #define LRS_SVT_JACOBI 2
+#define LRS_SVT_MULTI_WG 4
 size_t lrs_svt_workspace(int64_t P, int64_t B);
 int lrs_svt_f32(const float *X, const float *L2, float c2, int64_t P, int64_t B, double tau,
                 float *U, double *s_out, int warm, void *ws, size_t ws_bytes, void *stream);

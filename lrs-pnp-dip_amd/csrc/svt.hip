@@ -6,7 +6,7 @@
 //   2. warm start: A0 = V^T G V with the previous outer iteration's eigenvectors (tiled fp64
 //      GEMMs) — nearly diagonal, so Jacobi needs 1-3 sweeps instead of ~8;
 //   3. ONE workgroup runs a cyclic parallel (round-robin) two-sided Jacobi on A held in LDS as a
-//      packed fp64 upper triangle (B <= 200: <= 160,800 B), logging each round's rotations;
+//      packed fp64 upper triangle (B <= 198: <= 157,608 B), logging each round's rotations;
 //   4. the eigenvector update V <- V J_1 ... J_R is replayed from the log row by row in parallel
 //      (rows of V evolve independently), off the Jacobi workgroup's critical path;
 //   5. E = V diag(min(tau/s, 1)) V^T (fp64 -> f32) and U = Z - Z E.
@@ -25,7 +25,10 @@ namespace lrs {
 constexpr int kGramSlabs = 256;
 constexpr int kApSteps = 50;   // k-steps of 4 of the SVT apply: B <= 200
 constexpr int kJacobiThreads = 1024;
-constexpr int kMaxBp = 200;       // packed fp64 triangle of 200 x 200 = 160,800 B of LDS
+// packed fp64 triangle of 198 x 198 = 157,608 B of LDS, plus the solver's vectors and flags: at
+// Bp = 200 the one-workgroup chain would need 164,128 B (> 160 KiB), so B <= 198 (every reference
+// cube: 198 or 128 bands; LRS_E_UNSUPPORTED above)
+constexpr int kMaxBp = 198;
 constexpr int kMaxSweeps = 40;
 
 struct SvtWs {
@@ -451,20 +454,16 @@ namespace lrs {
 //     0.5 ||((lambda_j - lambda_i) (S - I)_ji)_j||, at most kEigRes * ||T||.
 // E = f(G) then differs from the exact matrix function by O(kEigRes ||T|| max|f'|).
 constexpr double kEigOrth0 = 0.05, kEigOrth = 1e-13, kEigRes = 1e-11;
-__global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double tau, int dbg) {
-    extern __shared__ double sm[];
-    __shared__ double shb[2], red[kEigThreads / 64];
-    const int n = (int)w.Bp, tid = threadIdx.x;
-    unsigned long long *ts = (unsigned long long *)(w.state + 16);   // phase timestamps (100 MHz)
-    if (tid == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
-    double *A = sm;
-    double *pv = A + (size_t)n * (n + 1) / 2;      // [n] p vector, then the eigenvalues
+
+// packed upper triangle of G (fp64, [n][n] in global) into LDS
+__device__ __forceinline__ void eig_load_packed(const double *G, double *A, int n) {
+    const int tid = threadIdx.x;
     for (int e0 = tid; e0 < n * n; e0 += 8 * kEigThreads) {
         double g[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int e = e0 + u * kEigThreads;
-            g[u] = e < n * n ? w.G[e] : 0.0;
+            g[u] = e < n * n ? G[e] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -472,45 +471,35 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double 
             if (e < n * n && j >= i) A[pk_idx(i, j, n)] = g[u];
         }
     }
-    __syncthreads();
-    eig_tridiag(A, pv, shb, n, w.beta);
-    if (tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
-    if (dbg)   // diagnostics: the tridiagonal T (d, e) into the Gram partial buffer
-        for (int j = tid; j < n; j += kEigThreads) {
-            const int idx = pk_idx(j, j, n);
-            w.partial[j] = A[idx];
-            w.partial[n + j] = (j + 1 < n) ? A[idx + 1] : 0.0;
-        }
-    // Gershgorin interval and the tridiagonal's scale (every thread, broadcast reads)
-    double gl = 1e300, gu = -1e300, emax2 = 0.0;
-    {
-        int idx = 0;
-        double ep = 0.0;
-        for (int j = 0; j < n; ++j) {
-            const double e = (j + 1 < n) ? fabs(A[idx + 1]) : 0.0;
-            gl = fmin(gl, A[idx] - ep - e);
-            gu = fmax(gu, A[idx] + ep + e);
-            emax2 = fmax(emax2, e * e);
-            ep = e;
-            if (j + 1 < n) idx += n - j;
-        }
+}
+
+// Gershgorin interval of T (diagonal / first superdiagonal of the packed A), its scale and the
+// Sturm pivot floor (every thread, broadcast reads)
+__device__ __forceinline__ void eig_bounds(const double *A, int n, double &gl, double &gu, double &tn, double &pivmin) {
+    gl = 1e300;
+    gu = -1e300;
+    double emax2 = 0.0;
+    int idx = 0;
+    double ep = 0.0;
+    for (int j = 0; j < n; ++j) {
+        const double e = (j + 1 < n) ? fabs(A[idx + 1]) : 0.0;
+        gl = fmin(gl, A[idx] - ep - e);
+        gu = fmax(gu, A[idx] + ep + e);
+        emax2 = fmax(emax2, e * e);
+        ep = e;
+        if (j + 1 < n) idx += n - j;
     }
-    const double tn = fmax(fmax(fabs(gl), fabs(gu)), 1e-300);
+    tn = fmax(fmax(fabs(gl), fabs(gu)), 1e-300);
     gl -= 4.0 * DBL_EPSILON * tn * n;
     gu += 4.0 * DBL_EPSILON * tn * n;
-    const double pivmin = 1e-290 * fmax(1.0, emax2);
-    eig_values(A, n, gl, gu, tn, pivmin, pv, w.lam);
-    __syncthreads();
-    if (tid == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
-    const double res = eig_vectors(A, pv, n, tn, w.F, w.T);
-    __syncthreads();
-    if (tid == 0) ts[3] = __builtin_amdgcn_s_memrealtime();
-    for (int k = tid; k < n - 2; k += kEigThreads) pv[k] = w.beta[k];   // the eigenvalues are in w.lam
-    __syncthreads();
-    eig_backtransform(A, pv, n, w.T, w.V[0]);
-    __syncthreads();
-    if (tid == 0) ts[4] = __builtin_amdgcn_s_memrealtime();
-    // certificate + orthogonalisation (LDS of the reflectors is free from here on)
+    pivmin = 1e-290 * fmax(1.0, emax2);
+}
+
+// D + F of the chain (one workgroup): the certificate on V = w.V[0], at most 3 Newton-Schulz
+// steps, the Jacobi fallback, then E.  res = this thread's eigenvector residual (thread i < n).
+__device__ __forceinline__ void eig_certify_finish(double *sm, double *red, const SvtWs &w, int n, int B, double tau,
+                                                   double tn, double res, int dbg, unsigned long long *ts) {
+    const int tid = threadIdx.x;
     int cur = 0;
     double dev = eig_syrk<true, 1>(sm, w.V[0], n, nullptr, 0.0, 0, nullptr, w.A0, red);
     bool bad = !(dev <= kEigOrth0);
@@ -532,7 +521,7 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double 
         dev = eig_syrk<true, 1>(sm, w.V[cur], n, nullptr, 0.0, 0, nullptr, w.A0, red);
     }
     bad = bad || !(dev <= kEigOrth);
-    if (tid == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
+    if (ts && tid == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
     if (dbg) {   // diagnostics: keep the tridiagonal path's V (no fallback, no E)
         if (tid == 0) { w.state[1] = cur; w.state[4] = bad ? 2 : 1; }
         return;
@@ -554,7 +543,98 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double 
     }
     __syncthreads();
     eig_syrk<false, 0>(sm, w.V[cur], n, w.lam, tau, B, w.E, nullptr, red, w.Fp);
-    if (tid == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
+    if (ts && tid == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
+}
+
+__global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double tau, int dbg) {
+    extern __shared__ double sm[];
+    __shared__ double shb[2], red[kEigThreads / 64];
+    const int n = (int)w.Bp, tid = threadIdx.x;
+    unsigned long long *ts = (unsigned long long *)(w.state + 16);   // phase timestamps (100 MHz)
+    if (tid == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
+    double *A = sm;
+    double *pv = A + (size_t)n * (n + 1) / 2;      // [n] p vector, then the eigenvalues
+    eig_load_packed(w.G, A, n);
+    __syncthreads();
+    eig_tridiag(A, pv, shb, n, w.beta);
+    if (tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
+    if (dbg)   // diagnostics: the tridiagonal T (d, e) into the Gram partial buffer
+        for (int j = tid; j < n; j += kEigThreads) {
+            const int idx = pk_idx(j, j, n);
+            w.partial[j] = A[idx];
+            w.partial[n + j] = (j + 1 < n) ? A[idx + 1] : 0.0;
+        }
+    double gl, gu, tn, pivmin;
+    eig_bounds(A, n, gl, gu, tn, pivmin);
+    eig_values(A, n, gl, gu, tn, pivmin, pv, w.lam);
+    __syncthreads();
+    if (tid == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
+    const double res = eig_vectors(A, pv, n, tn, w.F, w.T);
+    __syncthreads();
+    if (tid == 0) ts[3] = __builtin_amdgcn_s_memrealtime();
+    for (int k = tid; k < n - 2; k += kEigThreads) pv[k] = w.beta[k];   // the eigenvalues are in w.lam
+    __syncthreads();
+    eig_backtransform(A, pv, n, w.T, w.V[0]);
+    __syncthreads();
+    if (tid == 0) ts[4] = __builtin_amdgcn_s_memrealtime();
+    // certificate + orthogonalisation (LDS of the reflectors is free from here on)
+    eig_certify_finish(sm, red, w, n, B, tau, tn, res, dbg, ts);
+}
+
+// ---- 3''. the same chain over several workgroups (LRS_SVT_MULTI_WG) ---------------------------
+// Phases B (eigenvalues: 4 threads each), C (inverse iteration: a thread per eigenvector) and E
+// (back-transformation: a wave per 4 columns) are independent per eigenvalue / vector / column, so
+// they run on many CUs; A (tridiagonalisation) and D + F (certificate, fallback, E) stay on one
+// workgroup.  Every phase calls the device function k_svt_eig calls, with its workgroup's offset,
+// so the result is bit-identical.  For a caller whose chain is on the critical path (a row-slab
+// shard): beside a chip-filling sparse-coding kernel the one-workgroup chain is the
+// better choice (each launch here waits for free CUs).  Packed A (reflectors + T) passes through
+// w.A0 (free until the certificate), the residuals through w.partial.
+__global__ __launch_bounds__(kEigThreads) void k_svt_eig_tri(SvtWs w) {
+    extern __shared__ double sm[];
+    __shared__ double shb[2];
+    const int n = (int)w.Bp, tid = threadIdx.x;
+    double *A = sm;
+    double *pv = A + (size_t)n * (n + 1) / 2;
+    eig_load_packed(w.G, A, n);
+    __syncthreads();
+    eig_tridiag(A, pv, shb, n, w.beta);
+    __syncthreads();
+    const int np = n * (n + 1) / 2;
+    for (int e = tid; e < np; e += kEigThreads) w.A0[e] = A[e];
+}
+
+constexpr int kEigMwThreads = 64;   // one wave per workgroup for phases B and C (one per CU)
+
+__global__ __launch_bounds__(kEigMwThreads) void k_svt_eig_vals(SvtWs w) {
+    const int n = (int)w.Bp;
+    double gl, gu, tn, pivmin;
+    eig_bounds(w.A0, n, gl, gu, tn, pivmin);
+    eig_values(w.A0, n, gl, gu, tn, pivmin, w.lam, w.lam, kEigMwThreads * blockIdx.x);
+}
+
+__global__ __launch_bounds__(kEigMwThreads) void k_svt_eig_vecs(SvtWs w) {
+    const int n = (int)w.Bp;
+    double gl, gu, tn, pivmin;
+    eig_bounds(w.A0, n, gl, gu, tn, pivmin);
+    const double r = eig_vectors(w.A0, w.lam, n, tn, w.F, w.T, kEigMwThreads * blockIdx.x);
+    const int i = kEigMwThreads * blockIdx.x + threadIdx.x;
+    if (i < n) w.partial[i] = r;
+}
+
+__global__ __launch_bounds__(256) void k_svt_eig_back(SvtWs w) {
+    eig_backtransform(w.A0, w.beta, (int)w.Bp, w.T, w.V[0], 4 * blockIdx.x, 4 * gridDim.x);
+}
+
+__global__ __launch_bounds__(kEigThreads) void k_svt_eig_cert(SvtWs w, int B, double tau) {
+    extern __shared__ double sm[];
+    __shared__ double red[kEigThreads / 64];
+    const int n = (int)w.Bp, tid = threadIdx.x;
+    const double res = tid < n ? w.partial[tid] : 0.0;
+    double gl, gu, tn, pivmin;
+    eig_bounds(w.A0, n, gl, gu, tn, pivmin);   // from the packed A, before the certificate reuses A0
+    __syncthreads();
+    eig_certify_finish(sm, red, w, n, B, tau, tn, res, 0, nullptr);
 }
 
 // ---- 5a. E = V diag(e) V^T, e_k = min(tau/s_k, 1); s_out = sorted singular values -----------
@@ -761,11 +841,32 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
         const size_t tsmem = sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp);
         const size_t esmem = sizeof(double) * 2 * kEKc * kELd;
         const size_t lds = std::max(std::max(tsmem, esmem), std::max(smem, vsmem));
-        hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)lds);
-        if (ea != hipSuccess) return (int)ea;
-        hipLaunchKernelGGL(k_svt_eig, dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau, 0);
-        LRS_CHECK_LAUNCH();
+        if (warm & LRS_SVT_MULTI_WG) {
+            hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig_tri, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)tsmem);
+            if (ea == hipSuccess)
+                ea = hipFuncSetAttribute((const void *)k_svt_eig_cert, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds);
+            if (ea != hipSuccess) return (int)ea;
+            hipLaunchKernelGGL(k_svt_eig_tri, dim3(1), dim3(kEigThreads), tsmem, st, w);
+            LRS_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_svt_eig_vals, dim3((unsigned)((4 * Bp + kEigMwThreads - 1) / kEigMwThreads)),
+                               dim3(kEigMwThreads), 0, st, w);
+            LRS_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_svt_eig_vecs, dim3((unsigned)((Bp + kEigMwThreads - 1) / kEigMwThreads)),
+                               dim3(kEigMwThreads), 0, st, w);
+            LRS_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_svt_eig_back, dim3((unsigned)((Bp + 15) / 16)), dim3(256), 0, st, w);
+            LRS_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_svt_eig_cert, dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau);
+            LRS_CHECK_LAUNCH();
+        } else {
+            hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)lds);
+            if (ea != hipSuccess) return (int)ea;
+            hipLaunchKernelGGL(k_svt_eig, dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau, 0);
+            LRS_CHECK_LAUNCH();
+        }
     }
     if (s_out) {
         hipLaunchKernelGGL(k_sorted_singular_values, dim3(1), dim3(256), 0, st, w, (int)B, s_out);

@@ -211,8 +211,8 @@ __device__ __forceinline__ void sturm_rescale(double &p, double &pm) {
 // Sturm chains by readlane (no memory access inside the sequence).  The number of sign changes
 // of p_0 = 1, p_1(x), ..., p_n(x) is the number of eigenvalues below x.
 __device__ __noinline__ void eig_values(const double *A, int n, double gl, double gu, double tn, double pivmin,
-                                        double *lamv, double *lam_g) {
-    const int tid = threadIdx.x, lane = tid & 63;
+                                        double *lamv, double *lam_g, int tid0 = 0) {
+    const int tid = tid0 + (int)threadIdx.x, lane = tid & 63;   // tid0: this workgroup's first thread (multi-WG)
     double dr[4], er[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -275,8 +275,8 @@ __device__ __noinline__ void eig_values(const double *A, int n, double gl, doubl
 // global loads issued kEigUnroll rows ahead.  Returns ||T w_i - lambda_i w_i|| (0 for i >= n).
 constexpr int kEigUnroll = 4;
 __device__ __noinline__ double eig_vectors(const double *A, const double *lamv, int n, double tn, double *F,
-                                           double *W) {
-    const int i = threadIdx.x, lane = i & 63;
+                                           double *W, int tid0 = 0) {
+    const int i = tid0 + (int)threadIdx.x, lane = i & 63;
     double dr[4], er[4];   // d_j, e_j = A(j, j+1)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -381,10 +381,9 @@ __device__ __noinline__ double eig_vectors(const double *A, const double *lamv, 
 // ---- E. V = H_0 H_1 ... H_{n-3} W (V[j * n + c] = component j of eigenvector c) ----------------
 // beta_k from LDS (bl), reflector k from row k of the packed A.
 __device__ __noinline__ void eig_backtransform(const double *A, const double *bl, int n, const double *W,
-                                               double *V) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr int NW = kEigThreads / 64;
-    for (int c0 = 4 * wv; c0 < n; c0 += 4 * NW) {
+                                               double *V, int wave0 = 0, int nwaves = kEigThreads / 64) {
+    const int lane = threadIdx.x & 63, wv = wave0 + (int)(threadIdx.x >> 6);   // wave0 / nwaves: multi-WG
+    for (int c0 = 4 * wv; c0 < n; c0 += 4 * nwaves) {
         double x[4][4];
 #pragma unroll
         for (int c = 0; c < 4; ++c)

@@ -254,18 +254,21 @@ def svt_workspace(P: int, B: int, device) -> torch.Tensor:
     return torch.zeros(n, dtype=torch.uint8, device=device)
 
 
-SVT_WARM, SVT_JACOBI = 1, 2          # include/lrspnp.h flag word of the svt calls
+SVT_WARM, SVT_JACOBI, SVT_MULTI_WG = 1, 2, 4   # include/lrspnp.h flag word of the svt calls
 
 
-def _svt_flags(warm, method):
+def _svt_flags(warm, method, multi_wg=False):
     if method not in ("tri", "jacobi"):
         raise LrsError(f"unknown SVT eigensolver {method!r} (tri | jacobi)")
-    return (SVT_WARM if warm else 0) | (SVT_JACOBI if method == "jacobi" else 0)
+    return (SVT_WARM if warm else 0) | (SVT_JACOBI if method == "jacobi" else 0) | (SVT_MULTI_WG if multi_wg else 0)
 
 
-def svt(X, L2, c2: float, tau: float, ws, U=None, s_out=None, warm=False, stream=None, method="tri"):
+def svt(X, L2, c2: float, tau: float, ws, U=None, s_out=None, warm=False, stream=None, method="tri",
+        multi_wg=False):
     """U = SVT(X + c2*L2, tau) (main_LRS_PnP.py:118-124).  method 'tri': tridiagonal eigensolver
-    with a certified Jacobi fallback (default); 'jacobi': Jacobi only (warm-startable)."""
+    with a certified Jacobi fallback (default); 'jacobi': Jacobi only (warm-startable).  multi_wg:
+    the tridiagonal solver's eigenvalue / eigenvector / back-transformation phases over many
+    workgroups (LRS_SVT_MULTI_WG, bit-identical)."""
     L = device_lib()
     _dev(X, torch.float32, "X")
     if L2 is not None:
@@ -273,8 +276,8 @@ def svt(X, L2, c2: float, tau: float, ws, U=None, s_out=None, warm=False, stream
     P, B = X.shape
     if U is None:
         U = torch.empty_like(X)
-    check(L.lrs_svt_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out), _svt_flags(warm, method),
-                        _p(ws), ws.numel(), _s(stream)), "lrs_svt_f32")
+    check(L.lrs_svt_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out),
+                        _svt_flags(warm, method, multi_wg), _p(ws), ws.numel(), _s(stream)), "lrs_svt_f32")
     return U
 
 
@@ -295,12 +298,14 @@ def svt_gram_view(ws, P: int, B: int) -> torch.Tensor:
     return ws[off.value: off.value + 8 * n].view(torch.float64).view(ld.value, ld.value)
 
 
-def svt_finish(X, L2, c2: float, tau: float, ws, U, s_out=None, warm=False, stream=None, method="tri"):
-    """Second half of svt(): the one-workgroup eigensolver, E, then U = Z - Z E."""
+def svt_finish(X, L2, c2: float, tau: float, ws, U, s_out=None, warm=False, stream=None, method="tri",
+               multi_wg=False):
+    """Second half of svt(): the eigensolver (one workgroup, or multi_wg), E, then U = Z - Z E."""
     L = device_lib()
     P, B = X.shape
     check(L.lrs_svt_finish_f32(_p(X), _p(L2), float(c2), P, B, float(tau), _p(U), _p(s_out),
-                               _svt_flags(warm, method), _p(ws), ws.numel(), _s(stream)), "lrs_svt_finish_f32")
+                               _svt_flags(warm, method, multi_wg), _p(ws), ws.numel(), _s(stream)),
+          "lrs_svt_finish_f32")
     return U
 
 

@@ -34,6 +34,11 @@ class LrsPnPConfig:
     svt_method: str = "tri"       # SVT eigensolver: 'tri' (tridiagonal, certified) or 'jacobi'
     svt_warm: bool = True         # warm-start the Jacobi eigensolver from the previous iteration
     svt_gram_first: bool = False  # hold the sparse coding until the SVT Gram is done (always for Jacobi)
+    # The tridiagonal eigensolver's eigenvalue / inverse-iteration / back-transformation phases over
+    # many workgroups (LRS_SVT_MULTI_WG, bit-identical): "auto" on a row-slab shard, where the
+    # replicated solve is on the critical path; the one-workgroup chain beside a whole-cube sparse
+    # coding (a multi-launch chain there waits for free CUs between its launches).
+    svt_multi_wg: str = "auto"
     lowrank: str = "svt"          # 'svt' (main_LRS_PnP.py:315) or 'dip' (…1-LiP.py:399-411)
     dip: object = None            # lrspnp.dip.DipConfig for lowrank='dip' (None: reference defaults)
     dip_seed: int = 0             # DIP init seed of outer iteration t is dip_seed + t
@@ -270,8 +275,11 @@ class LrsPnP:
             self.comm.allreduce_(self.gram, lr)       # the cube's Gram = sum of the slabs' Grams
         gram_done = lr.record_event()
         # second half: the one-workgroup eigensolver then runs beside the sparse coding
+        mw = self.cfg.svt_multi_wg
+        if mw not in ("auto", "on", "off"):
+            raise LrsError(f"unknown svt_multi_wg {mw!r} (auto | on | off)")
         ops.svt_finish(self.X, self.L2, self.c2, self.tau, self.svt_ws, self.U, warm=warm, stream=lr,
-                       method=self.cfg.svt_method)
+                       method=self.cfg.svt_method, multi_wg=mw == "on" or (mw == "auto" and self.comm is not None))
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
                    stream=main)
         if self.cfg.svt_gram_first or self.cfg.svt_method == "jacobi":

@@ -68,6 +68,9 @@ def test_cover_ranges():
 
 def test_invalid_arguments_rejected():
     L = _lib.lib()
+    off, ld = ctypes.c_int64(), ctypes.c_int64()
+    assert L.lrs_svt_gram_offset(4000, 198, ctypes.byref(off), ctypes.byref(ld)) == 0 and ld.value == 198
+    assert L.lrs_svt_gram_offset(4000, 199, ctypes.byref(off), ctypes.byref(ld)) == -2   # B <= 198
     assert L.lrs_block_count(10, 10, 20, 20) < 0
     assert L.lrs_ista_f32(None, None, None, 64, 64, 256, 10, None, None, 10, 0, None, None, None, None, 0,
                           None) == -1

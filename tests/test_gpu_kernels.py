@@ -436,6 +436,33 @@ def test_svt_repeated_singular_values(ops, B, exact):
     assert rel(U, ref) < 1e-5
     path = ops.svt_state(ws, P, B)[4]
     assert path == (2 if exact else 1), path
+    # the multi-workgroup chain takes the same path and gives the same U bit for bit
+    Um = ops.svt(d(X), None, 1.0, float(np.float32(1 / 0.9)), ws, multi_wg=True).cpu().numpy()
+    assert ops.svt_state(ws, P, B)[4] == path and np.array_equal(Um.view(np.uint32), U.view(np.uint32))
+
+
+@pytest.mark.parametrize("P,B", [(1296, 128), (4000, 198), (500, 60), (777, 45), (300, 7), (2000, 197)])
+def test_svt_multi_workgroup_bit_identical(ops, P, B):
+    """LRS_SVT_MULTI_WG (the eigenvalue, inverse-iteration and back-transformation phases over many
+    workgroups, for a row-slab shard whose eigensolver is on the critical path): U and the singular
+    values bit-identical to the one-workgroup chain, on the tridiagonal path."""
+    rng = np.random.default_rng(3 * P + B)
+    Z = (rng.random((P, 6)) @ rng.random((6, B)) * 0.3 + 0.05 * rng.standard_normal((P, B)))
+    X = Z.astype(np.float32)
+    L2 = (0.01 * rng.standard_normal((P, B))).astype(np.float32)
+    c2 = np.float32(1 / 0.9)
+    tau = float(np.float32(1 / 0.9))
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    out = {}
+    for mw in (False, True):
+        ws = ops.svt_workspace(P, B, "cuda")
+        s = torch.empty(B, dtype=torch.float64, device="cuda")
+        U = ops.svt(d(X), d(L2), c2, tau, ws, s_out=s, multi_wg=mw).cpu().numpy()
+        out[mw] = (U, s.cpu().numpy(), ops.svt_state(ws, P, B)[4])
+    assert out[True][2] == out[False][2] == 1
+    assert np.array_equal(out[True][0].view(np.uint32), out[False][0].view(np.uint32))
+    assert np.array_equal(out[True][1], out[False][1])
+    assert rel(out[True][0], O.svt(X + c2 * L2, 1 / 0.9)) < 1e-5
 
 
 # ------------------------------------------------------------------------------------------ ADMM
