@@ -1134,6 +1134,7 @@ struct lrs_dipnet {
     // weight gradients run on a side stream beside the data-gradient chain (fork per conv node
     // after its BN backward, join before Adam)
     hipStream_t side = nullptr;
+    int side_prio = 0;   // the priority side was created with (the calling stream's)
     std::vector<hipEvent_t> ev_fork;
     hipEvent_t ev_join = nullptr;
     int64_t part2_off = 0;
@@ -1882,14 +1883,28 @@ extern "C" const float *lrs_dipnet_node_buffer(const lrs_dipnet *net, int node, 
 
 // The side stream and its fork/join events are created on the first training call (outside any
 // capture), so that creating a net and querying its layout needs no device.
-// The side stream takes the priority of the stream of that first call, so a caller that trains the
-// net on a high-priority stream (LrsPnPConfig.lowrank_priority) gets its weight gradients placed
-// with the same priority.
+// The side stream takes the priority of the calling stream, so a caller that trains the net on a
+// high-priority stream (LrsPnPConfig.lowrank_priority) gets its weight gradients placed with the
+// same priority; a call on a stream of another priority re-creates it (after the old one drains;
+// a captured graph that names it is dropped).
 static int ensure_side(lrs_dipnet *net, hipStream_t st) {
-    if (!net->fork_w || net->side) return LRS_OK;
+    if (!net->fork_w) return LRS_OK;
     int prio = 0;
     hipError_t e = hipStreamGetPriority(st, &prio);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&net->side, hipStreamNonBlocking, prio);
+    if (e != hipSuccess) return (int)e;
+    if (net->side) {
+        if (prio == net->side_prio) return LRS_OK;
+        drop_graph(net);
+        e = hipStreamSynchronize(net->side);
+        if (e == hipSuccess) e = hipStreamDestroy(net->side);
+        net->side = nullptr;
+        if (e != hipSuccess) return (int)e;
+        e = hipStreamCreateWithPriority(&net->side, hipStreamNonBlocking, prio);
+        if (e == hipSuccess) net->side_prio = prio;
+        return (int)e;
+    }
+    e = hipStreamCreateWithPriority(&net->side, hipStreamNonBlocking, prio);
+    if (e == hipSuccess) net->side_prio = prio;
     if (e == hipSuccess) e = hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming);
     for (size_t i = 0; i < net->ev_fork.size() && e == hipSuccess; ++i)
         e = hipEventCreateWithFlags(&net->ev_fork[i], hipEventDisableTiming);

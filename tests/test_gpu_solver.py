@@ -284,15 +284,18 @@ def test_task_parallel_dip_matches_one_rank(gpu, world):
     assert r["rel_X"] < 1e-6 and r["rel_L1"] < 1e-6 and r["rel_L2"] < 1e-6 and r["rel_U"] < 1e-6, r
 
 
-def test_lowrank_priority_same_iterates(gpu):
+@pytest.mark.parametrize("H", [36, 132])
+def test_lowrank_priority_same_iterates(gpu, H):
     """LrsPnPConfig.lowrank_priority only changes the queue priority of the DIP's streams (its
     training stream and the engine's weight-gradient side stream, which takes the same priority),
     not the arithmetic: two DIP solvers in one process, priority 0 and -1, same seeds, give the same
-    iterates (1e-6 relative L2, the task-parallel test's bar) after 2 outer iterations."""
+    iterates (1e-6 relative L2, the task-parallel test's bar) after 2 outer iterations.  132^2
+    (>= 16384 pixels) runs the weight gradients on the side stream; there one net is then also
+    trained on a stream of the other priority (the side stream is re-created) with equal results."""
     from lrspnp import LrsPnP, LrsPnPConfig
     from lrspnp.data import mask_matrix, synthetic_cube, synthetic_dictionary, unfold
     from lrspnp.dip import DipConfig
-    H, W, B, bb = 36, 36, 40, 12
+    W, B, bb = H, 40, 12
     obs, clean, mask = synthetic_cube(H, W, B, seed=5)
     Y, M = unfold(obs), mask_matrix(mask, B)
     Dct = synthetic_dictionary(bb * bb, 256, 0)
@@ -309,3 +312,13 @@ def test_lowrank_priority_same_iterates(gpu):
     (X0, U0), (X1, U1) = out
     assert float((X1 - X0).norm() / X0.norm()) < 1e-6
     assert float((U1 - U0).norm() / U0.norm()) < 1e-6
+    if H * W >= 16384:
+        # the same engine (priority -1 so far) trained on priority-0 / -1 / 0 streams
+        net = s.dip.net
+        res = []
+        for prio in (0, -1, 0):
+            net.stream = torch.cuda.Stream(priority=prio)
+            y = s.dip.run(s.dip_target, s.dip_in, s.dip_mask, seed=11, early_stop=False)
+            torch.cuda.synchronize()
+            res.append(y.clone())
+        assert torch.equal(res[0], res[1]) and torch.equal(res[0], res[2])

@@ -19,6 +19,8 @@ ap.add_argument("--bands", type=int, default=198)
 ap.add_argument("--steps", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--graph", action="store_true")
+ap.add_argument("--dump", default=None, help="also save the net output after the timed rounds (.npy): "
+                                              "bit-for-bit A/B of output-preserving kernel changes")
 a = ap.parse_args()
 net = DipNet(lipschitz_unet_nodes(a.bands, a.bands, 128), a.bands, a.hw, a.hw)
 net.init_params(0)
@@ -37,3 +39,6 @@ for r in range(a.rounds):
     torch.cuda.synchronize()
     res.append(e0.elapsed_time(e1) / a.steps)
 print("dip step ms:", " ".join(f"{v:.4f}" for v in res), "median", f"{statistics.median(res):.4f}")
+if a.dump:
+    import numpy as np
+    np.save(a.dump, net.output().detach().cpu().numpy())
