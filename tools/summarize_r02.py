@@ -8,7 +8,7 @@ Per workload <wl> in {dip, pnp} (whatever was profiled):
   <wl>_summary.json       per-kernel mean duration (trace), HBM bytes (PMC), SQ counters
 and traffic.json (read by bench.py for roofline.traffic):
   dip_hbm_bytes_per_outer_iter       sum over the DIP prox's kernels / outer iterations profiled
-  dip_ista_hbm_bytes_per_launch      k_ista_rs, mean per launch
+  dip_ista_hbm_bytes_per_launch      the sparse-coding kernel (k_ista_pat, or k_ista_rs), mean per launch
   pnp_ista_hbm_bytes_per_launch      k_ista_ln2, mean per launch
 
 HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE for every kernel (MI355X_MICROARCH.md §HBM: on gfx950
@@ -26,7 +26,7 @@ from collections import defaultdict
 
 src, dst = sys.argv[1], sys.argv[2]
 os.makedirs(dst, exist_ok=True)
-NOT_DIP = ("k_ista", "k_admm_update", "k_alpha", "k_psnr", "at::native", "__amd_rocclr", "k_ssim")
+NOT_DIP = ("k_ista", "k_pat_gram", "k_admm_update", "k_alpha", "k_psnr", "at::native", "__amd_rocclr", "k_ssim")
 
 
 def kname(r):
@@ -86,7 +86,7 @@ for wl in ("dip", "pnp"):
         if wl == "dip" and is_dip(k):
             dip_bytes += 2 * f + w
             dip_ms += sum(v)
-    ista = [k for k in dur if "k_ista_rs<" in k or "k_ista_ln2<" in k]
+    ista = [k for k in dur if "k_ista_pat<" in k or "k_ista_rs<" in k or "k_ista_ln2<" in k]
     summ = {"workload": wl, "outer_iterations_profiled": outer, "kernels": kern}
     if ista:
         k = ista[0]
