@@ -363,8 +363,9 @@ def main_dip(args, ctx):
     n = bb * bb
     pat = getattr(s, "pat_plan", None) is not None
     # matrix-core work per launch: the row-split kernel's two products per iteration (+ Phi), or the
-    # per-pattern path's Grams, b and Phi once and one K x K product per iteration
-    ista_flops = (s.npat * 2 * n * args.K ** 2 + s.nb * (4 * n * args.K + nit * 2 * args.K ** 2) if pat else
+    # per-pattern path's b and Phi once and one K x K product per iteration (its Grams are formed
+    # once per solve, lrs_ista_pat_prepare, outside the timed steps)
+    ista_flops = (s.nb * (4 * n * args.K + nit * 2 * args.K ** 2) if pat else
                   nit * s.nb * 4 * n * args.K + s.nb * 2 * n * args.K)
     ista_name = (f"k_ista_pat (lrs_ista_pat_f32: {s.nb} blocks of {n} rows in {s.pat_ntiles} tiles of "
                  f"{s.npat} observation patterns, Nit {nit}" if pat else

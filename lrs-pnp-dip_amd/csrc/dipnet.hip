@@ -1544,10 +1544,11 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     auto fail = [&](int rc) { delete net; return rc; };
     net->opts = o;
     net->implicit = o.precision == LRS_DIP_SPLIT_BF16;
-    // weight gradients on a side stream from 128^2 up: neutral alone at 196^2, but beside the
-    // concurrent sparse-coding kernel the second stream keeps the DIP its share of the chip
-    // (configs[2] 4.73 -> 5.19 outer it/s); slower at 36^2 (1.03 -> 1.19 ms per step)
-    net->fork_w = (int64_t)H * W >= 16384;
+    // weight gradients on a side stream at every size: beside the concurrent sparse-coding kernel
+    // the second stream keeps the DIP its share of the chip (configs[2] 4.73 -> 5.19 outer it/s,
+    // round 1); at 36^2 it was slower in round 1 (1.03 -> 1.19 ms per step) and is faster since the
+    // small-map fork points pair up (round 4, interleaved: 0.729 -> 0.676 ms per step)
+    net->fork_w = true;
     net->fork_w = tune_knob("LRS_DIP_FORK", net->fork_w ? 1 : 0) != 0;   // tuning build only
     int64_t pofs = 0, rofs = 0, ofs = 0, max_dz = 0, max_dcol = 0, part = 0, max_bnpart = 0;
     int n_sn = 0;

@@ -6,6 +6,8 @@ o=gpurun_out/r04n
 mkdir -p $o
 export TMPDIR=/tmp
 TL=$PWD/lrs-pnp-dip_amd/lrspnp/liblrspnp_hip_tune.so
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1 || { tail $o/smoke.log; exit 1; }
+tail -1 $o/smoke.log
 for r in 1 2; do
   for f in 0 1; do
     for gr in "" "--graph"; do
