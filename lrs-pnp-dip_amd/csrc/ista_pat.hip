@@ -124,14 +124,16 @@ struct IstaPatParams {
 // gradient rows [16 blocks][KP] read by the prox (chunk index XOR-swizzled by block)
 __host__ __device__ constexpr size_t pat_lds_bytes(int NQ) { return (size_t)NQ * 2048; }
 
-template <int NQ, int S>
-__global__ __launch_bounds__(64 * S) void k_ista_pat(IstaPatParams p) {
+// WPE: waves per SIMD the registers are bounded for (2: one 512-thread workgroup per CU; 4: two)
+template <int NQ, int S, int WPE = 2>
+__global__ __launch_bounds__(64 * S, WPE) void k_ista_pat(IstaPatParams p) {
     static_assert(NQ % S == 0, "atom tiles split evenly over the waves");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int KP = NQ * 16;
     constexpr int NOWN = NQ / S;                  // atom tiles per wave
     constexpr int NFRAG = NQ * NOWN;              // Q fragments per wave and iteration
-    constexpr int RING = NFRAG < 8 ? NFRAG : 8;
+    constexpr int RMAX = WPE > 2 ? 4 : 8;
+    constexpr int RING = NFRAG < RMAX ? NFRAG : RMAX;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int jl = lane & 15, g = lane >> 4;
@@ -337,20 +339,24 @@ static int pat_waves_knob() {
     const char *e = getenv("LRS_ISTA_PAT_WAVES");
     return e ? atoi(e) : 0;
 }
+static int pat_wpe_knob() {   // LRS_ISTA_PAT_WPE=2: the unbounded-register form (one workgroup per CU)
+    const char *e = getenv("LRS_ISTA_PAT_WPE");
+    return e ? atoi(e) : 0;
+}
 #endif
 
-template <int NQ, int S>
+template <int NQ, int S, int WPE = 2>
 static int launch_pat_k(const IstaPatParams &p, int64_t max_wg, hipStream_t st) {
     static bool lds_opt_in = false;
     if (!lds_opt_in) {
-        const hipError_t e =
-            hipFuncSetAttribute((const void *)k_ista_pat<NQ, S>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        const hipError_t e = hipFuncSetAttribute((const void *)k_ista_pat<NQ, S, WPE>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return (int)e;
         lds_opt_in = true;
     }
     int64_t grid = p.ntiles;
     if (max_wg > 0 && grid > max_wg) grid = max_wg;
-    hipLaunchKernelGGL((k_ista_pat<NQ, S>), dim3((unsigned)grid), dim3(64 * S), pat_lds_bytes(NQ), st, p);
+    hipLaunchKernelGGL((k_ista_pat<NQ, S, WPE>), dim3((unsigned)grid), dim3(64 * S), pat_lds_bytes(NQ), st, p);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -400,7 +406,14 @@ int ista_pat_launch(const float *Yb, const uint8_t *obs_pat, int64_t npat, const
     switch (NQ) {
     case 4: return launch_pat_k<4, 4>(p, max_wg, st);
     case 8: return launch_pat_k<8, 4>(p, max_wg, st);
-    case 16: return waves == 8 ? launch_pat_k<16, 8>(p, max_wg, st) : launch_pat_k<16, 4>(p, max_wg, st);
+    case 16:
+        // 8 waves bounded to 128 registers (4 waves per SIMD: two workgroups per CU, one's prox beside
+        // the other's products): bit-identical, configs[3]'s sparse coding 11.3 -> 10.6 ms, configs[2]'s
+        // beside the DIP 1.745 -> 1.683 ms (profiles/r04/ista_pat_wpe/)
+#ifdef LRS_TUNING
+        if (waves == 8 && pat_wpe_knob() == 2) return launch_pat_k<16, 8>(p, max_wg, st);
+#endif
+        return waves == 8 ? launch_pat_k<16, 8, 4>(p, max_wg, st) : launch_pat_k<16, 4>(p, max_wg, st);
     default: return launch_pat_k<32, 8>(p, max_wg, st);
     }
 }
