@@ -233,7 +233,11 @@ class LrsPnP:
             return
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d[b0:b1], self.cols_d[b0:b1], self.n_pad,
                    Yb=self.Yb[b0:b1], stream=stream)
-        ws = self.ista_ws if self.pat_plan is None else None   # a block range runs the row-split kernel
+        ws = self.ista_ws
+        if self.pat_plan is not None:   # a block range runs the row-split kernel, on a workspace of its own
+            if getattr(self, "_rs_ws", None) is None:
+                self._rs_ws = ops.ista_workspace(self.n, self.K, self.prox, self.Yb.device)
+            ws = self._rs_ws
         ops.ista(self.Yb[b0:b1], self.obs[b0:b1], self.D, self.n, self.alpha[b0:b1], self.thr[b0:b1], self.cfg.Nit,
                  self.prox, phi=self.phi[b0:b1], ws=ws, stream=stream)
 
