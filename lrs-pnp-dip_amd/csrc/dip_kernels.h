@@ -841,23 +841,34 @@ __device__ __forceinline__ float bn_act_bwd(float g, float xh, float gm, float b
     return act_bwd(g, y, a.act);
 }
 
-__device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int sb, double (&o)[3], double *red) {
+// redf: the Lipschitz scale's reduction scratch (kBn*Threads / 64 floats); with beta the LeakyReLU
+// branch comes from the pre-activation (bn_act_bwd), so y is not read
+__device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int sb, double (&o)[3], double *red,
+                                                  float *redf) {
     const int64_t off = (int64_t)c * a.P;
     const float *gy = a.gy + off, *y = a.y + off, *z = a.z + off;
     const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
     double sg = 0.0, sgx = 0.0, sx = 0.0;
+    const bool ldy = bn_needs_y(a);
+    float gm = 0.0f, bt = 0.0f;
+    if (a.bn && !ldy) {
+        const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+        gm = a.gamma[c] / cs;
+        bt = a.beta[c] / cs;
+    }
     if (a.bn && a.vec) {
         const float m32 = a.mean[c], is32 = a.invstd[c];
         const float4 *gy4 = reinterpret_cast<const float4 *>(gy), *y4 = reinterpret_cast<const float4 *>(y),
                      *z4 = reinterpret_cast<const float4 *>(z);
         for (int q = (i0 >> 2) + threadIdx.x; q < (i1 >> 2); q += blockDim.x) {
-            const float4 gv = gy4[q], yv = y4[q], zv = z4[q];
+            const float4 gv = gy4[q], zv = z4[q];
+            const float4 yv = ldy ? y4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
             const float ge[4] = {gv.x, gv.y, gv.z, gv.w}, ye[4] = {yv.x, yv.y, yv.z, yv.w},
                         ze[4] = {zv.x, zv.y, zv.z, zv.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float g = act_bwd(ge[e], ye[e], a.act);
                 const float xh = (ze[e] - m32) * is32;
+                const float g = ldy ? act_bwd(ge[e], ye[e], a.act) : bn_act_bwd(ge[e], xh, gm, bt, 0.0f, a);
                 sg += (double)g;
                 sgx += (double)g * (double)xh;
                 sx += (double)xh;
@@ -866,8 +877,8 @@ __device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int
     } else if (a.bn) {
         const float m32 = a.mean[c], is32 = a.invstd[c];
         for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-            const float g = act_bwd(gy[i], y[i], a.act);
             const float xh = (z[i] - m32) * is32;
+            const float g = ldy ? act_bwd(gy[i], y[i], a.act) : bn_act_bwd(gy[i], xh, gm, bt, 0.0f, a);
             sg += (double)g;
             sgx += (double)g * (double)xh;
             sx += (double)xh;
@@ -883,9 +894,10 @@ __device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int
 
 __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
     __shared__ double red[2 * kBnThreads / 64];
+    __shared__ float redf[kBnThreads / 64];
     const int c = blockIdx.y, sb = blockIdx.x;
     double o[3];
-    bn_bwd_stats_body(a, c, sb, o, red);
+    bn_bwd_stats_body(a, c, sb, o, red, redf);
     if (threadIdx.x == 0) {
         double *pp = a.part + ((int64_t)c * a.S + sb) * 3;
         pp[0] = o[0];
@@ -913,6 +925,8 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnBwdArgs &a, int c, int
     const float m32 = a.mean[c], is32 = a.invstd[c];
     const float gm = a.gamma[c] / cs;
     const float k = gm * is32;
+    const bool ldy = bn_needs_y(a);
+    const float bt = ldy ? 0.0f : a.beta[c] / cs;
     if (threadIdx.x == 0) {
         const float mg = (float)(t[0] / a.P), mgx = (float)(t[1] / a.P);
         st_s[0] = mg;
@@ -931,14 +945,15 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnBwdArgs &a, int c, int
                      *z4 = reinterpret_cast<const float4 *>(z);
         float4 *gz4 = reinterpret_cast<float4 *>(gz);
         for (int q = (i0 >> 2) + threadIdx.x; q < (i1 >> 2); q += blockDim.x) {
-            const float4 gv = gy4[q], yv = y4[q], zv = z4[q];
+            const float4 gv = gy4[q], zv = z4[q];
+            const float4 yv = ldy ? y4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
             const float ge[4] = {gv.x, gv.y, gv.z, gv.w}, ye[4] = {yv.x, yv.y, yv.z, yv.w},
                         ze[4] = {zv.x, zv.y, zv.z, zv.w};
             float o[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float g = act_bwd(ge[e], ye[e], a.act);
                 const float xh = (ze[e] - m32) * is32;
+                const float g = ldy ? act_bwd(ge[e], ye[e], a.act) : bn_act_bwd(ge[e], xh, gm, bt, 0.0f, a);
                 o[e] = k * (g - mg - xh * mgx);
             }
             float4 r = make_float4(o[0], o[1], o[2], o[3]);
@@ -951,8 +966,8 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnBwdArgs &a, int c, int
         return;
     }
     for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const float g = act_bwd(gy[i], y[i], a.act);
         const float xh = (z[i] - m32) * is32;
+        const float g = ldy ? act_bwd(gy[i], y[i], a.act) : bn_act_bwd(gy[i], xh, gm, bt, 0.0f, a);
         const float v = k * (g - mg - xh * mgx);
         gz[i] = a.accum ? gz[i] + v : v;
     }
@@ -978,7 +993,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd1(BnBwdArgs a) {
     __shared__ float st_s[2];
     const int c = blockIdx.y;
     double o[3];
-    bn_bwd_stats_body(a, c, 0, o, red);
+    bn_bwd_stats_body(a, c, 0, o, red, redf);
     const double t[3] = {0.0 + o[0], 0.0 + o[1], 0.0 + o[2]};
     bn_bwd_apply_body(a, c, 0, t, redf, st_s);
 }

@@ -1478,12 +1478,13 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
             if (t > 0) {
                 rc = bn_bwd(gout, outp, net->tensor(t, x), net->params + N.gm_off, net->f(N.mean_off),
                             net->f(N.istd_off), net->f(net->nodes[t - 1].grad_off), net->grads + N.gm_off,
-                            net->grads + N.bt_off, nullptr, N.C, N.P, N.d.act, net->bnpart(), st, lip, written[t]);
+                            net->grads + N.bt_off, nullptr, N.C, N.P, N.d.act, net->bnpart(), st, lip, written[t],
+                            net->params + N.bt_off);
                 written[t] = 1;
             } else {   // BN straight on the input: parameter grads only
                 rc = bn_bwd(gout, outp, net->tensor(t, x), net->params + N.gm_off, net->f(N.mean_off),
                             net->f(N.istd_off), net->f(net->dz_off), net->grads + N.gm_off, net->grads + N.bt_off,
-                            nullptr, N.C, N.P, N.d.act, net->bnpart(), st, lip, 0);
+                            nullptr, N.C, N.P, N.d.act, net->bnpart(), st, lip, 0, net->params + N.bt_off);
             }
             if (rc) return rc;
         } else {

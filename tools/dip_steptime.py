@@ -11,7 +11,7 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lrs-pnp-dip_amd"))
 import torch  # noqa: E402
-from lrspnp.dip import DipNet, lipschitz_unet_nodes  # noqa: E402
+from lrspnp.dip import DipNet, lipschitz_unet_nodes, skip_nodes  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--hw", type=int, default=196)
@@ -19,10 +19,13 @@ ap.add_argument("--bands", type=int, default=198)
 ap.add_argument("--steps", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--graph", action="store_true")
+ap.add_argument("--net", default="unet", choices=["unet", "skip"], help="the 1-Lip U-Net (configs[2]) or the skip "
+                                                                          "net (configs[3])")
 ap.add_argument("--dump", default=None, help="also save the net output after the timed rounds (.npy): "
                                               "bit-for-bit A/B of output-preserving kernel changes")
 a = ap.parse_args()
-net = DipNet(lipschitz_unet_nodes(a.bands, a.bands, 128), a.bands, a.hw, a.hw)
+nodes = lipschitz_unet_nodes(a.bands, a.bands, 128) if a.net == "unet" else skip_nodes(a.bands, a.bands)
+net = DipNet(nodes, a.bands, a.hw, a.hw)
 net.init_params(0)
 g = torch.Generator(device="cuda").manual_seed(0)
 x = torch.rand(a.bands, a.hw, a.hw, device="cuda", generator=g)
