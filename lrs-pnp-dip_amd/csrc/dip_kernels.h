@@ -2026,6 +2026,88 @@ __global__ void k_concat_fwd(const float *__restrict__ a, const float *__restric
     }
 }
 
+// The same copies / sums laid out for throughput: grid (row quads, channels), a thread = 4
+// consecutive x of one row of one channel; no 64-bit division per element, float4 stores when the
+// rows are multiples of 4 (the values and the 2x2 summation order are k_concat_fwd / _bwd's).
+__global__ __launch_bounds__(256) void k_concat_fwd4(const float *__restrict__ a, const float *__restrict__ b,
+                                                     CatGeom g, float *__restrict__ out) {
+    const int W4 = (g.W + 3) >> 2;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= g.H * W4) return;
+    const int c = blockIdx.y, y = t / W4, x0 = 4 * (t - y * W4);
+    float v[4];
+    if (c < g.Ca) {
+        const float *src = a + ((int64_t)c * g.Ha + y + g.oay) * g.Wa + g.oax;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = x0 + e < g.W ? src[x0 + e] : 0.0f;
+    } else {
+        int yy = y + g.oby;
+        if (g.upb) yy >>= 1;
+        const float *src = b + ((int64_t)(c - g.Ca) * g.Hb + yy) * g.Wb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            int xx = x0 + e + g.obx;
+            if (g.upb) xx >>= 1;
+            v[e] = x0 + e < g.W ? src[xx] : 0.0f;
+        }
+    }
+    float *dst = out + ((int64_t)c * g.H + y) * g.W + x0;
+    if ((g.W & 3) == 0) {
+        *reinterpret_cast<float4 *>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (x0 + e < g.W) dst[e] = v[e];
+    }
+}
+
+// part 0: ga over (Ha rows x Wa), channels Ca; part 1: gb over (Hb x Wb), channels Cb
+__global__ __launch_bounds__(256) void k_concat_bwd4(const float *__restrict__ go, CatGeom g, float *__restrict__ gx,
+                                                     int acc, int part) {
+    const int Hs = part ? g.Hb : g.Ha, Ws = part ? g.Wb : g.Wa;
+    const int W4 = (Ws + 3) >> 2;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= Hs * W4) return;
+    const int c = blockIdx.y, Y = t / W4, X0 = 4 * (t - Y * W4);
+    const int64_t HW = (int64_t)g.H * g.W;
+    float v[4];
+    if (part == 0) {
+        const float *gc = go + (int64_t)c * HW;
+        const int y = Y - g.oay;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int x = X0 + e - g.oax;
+            v[e] = (y >= 0 && y < g.H && x >= 0 && x < g.W && X0 + e < Ws) ? gc[(int64_t)y * g.W + x] : 0.0f;
+        }
+    } else {
+        const float *gc = go + (int64_t)(g.Ca + c) * HW;
+        const int f = g.upb ? 2 : 1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float s = 0.0f;
+            for (int dy = 0; dy < f; ++dy)
+                for (int dx = 0; dx < f; ++dx) {
+                    const int y = Y * f + dy - g.oby, x = (X0 + e) * f + dx - g.obx;
+                    if (y >= 0 && y < g.H && x >= 0 && x < g.W) s += gc[(int64_t)y * g.W + x];
+                }
+            v[e] = s;
+        }
+    }
+    float *dst = gx + ((int64_t)c * Hs + Y) * Ws + X0;
+    if ((Ws & 3) == 0) {
+        float4 r = make_float4(v[0], v[1], v[2], v[3]);
+        if (acc) {
+            const float4 o = *reinterpret_cast<const float4 *>(dst);
+            r = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
+        }
+        *reinterpret_cast<float4 *>(dst) = r;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (X0 + e < Ws) dst[e] = acc ? dst[e] + v[e] : v[e];
+    }
+}
+
 // ga (nullable) / gb (nullable): gather the output gradient back (zeros outside the crop;
 // the 2x2 children of an upsampled b pixel are summed); accumulate flags per input
 __global__ void k_concat_bwd(const float *__restrict__ go, CatGeom g, float *__restrict__ ga, int acc_a,

@@ -1255,9 +1255,10 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
                         net->f(N.mean_off), net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C,
                         N.C, N.P, N.d.act, 1e-5f, 0.1f, net->bnpart(), st, lip);
         } else {
-            const int64_t n = (int64_t)N.C * N.P;
-            hipLaunchKernelGGL(k_concat_fwd, dim3(ew_blocks(n, 1 << 16)), dim3(kEw), 0, st, net->tensor(N.d.in0, x),
-                               net->tensor(N.d.in1, x), N.cg, out);
+            const int q = N.cg.H * ((N.cg.W + 3) / 4);
+            if (N.cg.Ca + N.cg.Cb > 65535 || !al16(out)) return LRS_E_UNSUPPORTED;
+            hipLaunchKernelGGL(k_concat_fwd4, dim3((unsigned)((q + 255) / 256), (unsigned)(N.cg.Ca + N.cg.Cb)), dim3(256),
+                               0, st, net->tensor(N.d.in0, x), net->tensor(N.d.in1, x), N.cg, out);
             rc = LRS_OK;
         }
         if (rc) return rc;
@@ -1497,14 +1498,19 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
                 const int acc_a = ta > 0 ? written[ta] : 0;
                 // both inputs may be the same tensor: the b pass must then accumulate onto the a pass
                 const int acc_b = tb > 0 ? (written[tb] || (tb == ta)) : 0;
-                if (ta == tb && ga) {
-                    hipLaunchKernelGGL(k_concat_bwd, dim3(ew_blocks(na, 1 << 16)), dim3(kEw), 0, st, gout, N.cg, ga,
-                                       acc_a, nullptr, 0);
-                    hipLaunchKernelGGL(k_concat_bwd, dim3(ew_blocks(nb, 1 << 16)), dim3(kEw), 0, st, gout, N.cg,
-                                       nullptr, 0, gb, 1);
-                } else {
-                    hipLaunchKernelGGL(k_concat_bwd, dim3(ew_blocks(na + nb, 1 << 16)), dim3(kEw), 0, st, gout, N.cg,
-                                       ga, acc_a, gb, acc_b);
+                // a then b (the same order as one launch over both when ta == tb)
+                const CatGeom &cg = N.cg;
+                if (ga) {
+                    if (!al16(ga)) return LRS_E_UNSUPPORTED;
+                    const int q = cg.Ha * ((cg.Wa + 3) / 4);
+                    hipLaunchKernelGGL(k_concat_bwd4, dim3((unsigned)((q + 255) / 256), (unsigned)cg.Ca), dim3(256), 0,
+                                       st, gout, cg, ga, acc_a, 0);
+                }
+                if (gb) {
+                    if (!al16(gb)) return LRS_E_UNSUPPORTED;
+                    const int q = cg.Hb * ((cg.Wb + 3) / 4);
+                    hipLaunchKernelGGL(k_concat_bwd4, dim3((unsigned)((q + 255) / 256), (unsigned)cg.Cb), dim3(256), 0,
+                                       st, gout, cg, gb, (ta == tb && ga) ? 1 : acc_b, 1);
                 }
             }
             if (ta > 0) written[ta] = 1;
