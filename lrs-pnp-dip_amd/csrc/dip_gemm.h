@@ -1210,4 +1210,36 @@ __global__ __launch_bounds__(256) void k_fold_pad(const float *__restrict__ gxp,
     }
 }
 
+// k_fold_pad for one partial (nsplit == 1, no upsample; a data-gradient GEMM with enough tiles, e.g.
+// the 512^2 layers of configs[3]): grid (row quads, Cin), a thread = 4 consecutive source x of one
+// row, float4 stores (Ws % 4 == 0).  Per pixel the same padded sources in the same order as
+// k_fold_pad, so the result is bit-identical.
+__global__ __launch_bounds__(256) void k_fold_pad1q(const float *__restrict__ gxp, ConvGeom gm, float *__restrict__ gx,
+                                                    int accum) {
+    const int W4 = gm.Ws >> 2, Wp = gm.Wu + 2 * gm.pad, Qp = (gm.Hu + 2 * gm.pad) * Wp;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= gm.Hs * W4) return;
+    const int c = blockIdx.y, sy = t / W4, sx0 = 4 * (t - sy * W4);
+    const float *src = gxp + (int64_t)c * Qp;
+    int iys[3];
+    const int ny = padded_sources(sy, gm.Hu, gm.pad, gm.pad_mode, iys);
+    float acc[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        int ixs[3];
+        const int nx = padded_sources(sx0 + e, gm.Wu, gm.pad, gm.pad_mode, ixs);
+        float a = 0.0f;
+        for (int py = 0; py < ny; ++py)
+            for (int px = 0; px < nx; ++px) a += src[iys[py] * Wp + ixs[px]];
+        acc[e] = a;
+    }
+    float4 *o = reinterpret_cast<float4 *>(gx + ((int64_t)c * gm.Hs + sy) * gm.Ws + sx0);
+    float4 r = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    if (accum) {
+        const float4 p = *o;
+        r = make_float4(p.x + r.x, p.y + r.y, p.z + r.z, p.w + r.w);
+    }
+    *o = r;
+}
+
 }  // namespace lrs

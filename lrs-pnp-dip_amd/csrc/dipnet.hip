@@ -671,9 +671,15 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
                           LdDgradTM{gz, Cout * P * 4, g, Cout, Cop, nullptr}, dcol, nullptr, nullptr, g.Cin, Qp,
                           kk * Cop, part, part_cap, st, &nsplit, 0, dgrad_split_target());
         if (rc) return rc;
-        const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
-        hipLaunchKernelGGL(k_fold_pad, grid, dim3(256), 0, st, nsplit > 1 ? part : dcol, nsplit, (int64_t)g.Cin * Qp, g,
-                           gx, accum_gx);
+        if (nsplit == 1 && !g.up && g.Ws % 4 == 0 && g.Cin <= 65535 && ((uintptr_t)gx & 15) == 0) {   // one partial: row quads
+            const int q = g.Hs * (g.Ws / 4);
+            hipLaunchKernelGGL(k_fold_pad1q, dim3((unsigned)((q + 255) / 256), (unsigned)g.Cin), dim3(256), 0, st, dcol,
+                               g, gx, accum_gx);
+        } else {
+            const dim3 grid((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535));
+            hipLaunchKernelGGL(k_fold_pad, grid, dim3(256), 0, st, nsplit > 1 ? part : dcol, nsplit, (int64_t)g.Cin * Qp,
+                               g, gx, accum_gx);
+        }
         LRS_CHECK_LAUNCH();
         return LRS_OK;
     }
