@@ -45,7 +45,9 @@ class LrsPnPConfig:
     # Workgroups of the sparse-coding kernel beside the DIP training (lowrank='dip';
     # lrs_ista_opts.max_workgroups, 0 = one per 16-block tile).  Measured at configs[2]
     # (bench.py --ista-max-wg): 0 -> 7.25 outer it/s, 128 -> 7.18, 64 -> 6.97, 32 -> 6.68: a longer,
-    # narrower sparse coding taxes the DIP more than a short full-chip one, so unbounded.
+    # narrower sparse coding taxes the DIP more than a short full-chip one, so unbounded.  Re-measured
+    # on the per-pattern kernel (405 tiles, 3 interleaved rounds, profiles/r04/ista_max_wg/):
+    # 0 -> 7.85 / 7.84 / 7.84, 256 -> 7.84 / 7.84 / 7.82, 128 -> 7.80 / 7.81 / 7.80.
     ista_max_wg_dip: int = 0
     # Launches the sparse coding's Nit iterations are split over beside the DIP training
     # (lowrank='dip'; lrs_ista_opts.warm_start: the iterates are exactly those of one launch).  A
