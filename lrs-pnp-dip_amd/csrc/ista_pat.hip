@@ -339,7 +339,7 @@ static int pat_waves_knob() {
     const char *e = getenv("LRS_ISTA_PAT_WAVES");
     return e ? atoi(e) : 0;
 }
-static int pat_wpe_knob() {   // LRS_ISTA_PAT_WPE=2: the unbounded-register form (one workgroup per CU)
+static int pat_wpe_knob() {   // LRS_ISTA_PAT_WPE=4: the 128-register form (two workgroups per CU)
     const char *e = getenv("LRS_ISTA_PAT_WPE");
     return e ? atoi(e) : 0;
 }
@@ -407,13 +407,16 @@ int ista_pat_launch(const float *Yb, const uint8_t *obs_pat, int64_t npat, const
     case 4: return launch_pat_k<4, 4>(p, max_wg, st);
     case 8: return launch_pat_k<8, 4>(p, max_wg, st);
     case 16:
-        // 8 waves bounded to 128 registers (4 waves per SIMD: two workgroups per CU, one's prox beside
-        // the other's products): bit-identical, configs[3]'s sparse coding 11.3 -> 10.6 ms, configs[2]'s
-        // beside the DIP 1.745 -> 1.683 ms (profiles/r04/ista_pat_wpe/)
+        // 8 waves, registers unbounded (192, one workgroup per CU).  The 128-register bound (two
+        // workgroups per CU; LRS_ISTA_PAT_WPE=4, tuning build) is bit-identical and a little faster
+        // (configs[3]'s sparse coding 11.3 -> 10.6 ms, configs[2]'s beside the DIP 1.745 -> 1.683 ms;
+        // the configs[2] bench 7.87 either way, profiles/r04/ista_pat_wpe/), but spills 37 registers
+        // (152 B of scratch per lane, 29 with a 2-deep ring): the PMC pass then measured 1.26 GB of
+        // fabric traffic per configs[2] launch instead of 122 MB (profiles/r04/ista_pat_spill/).
 #ifdef LRS_TUNING
-        if (waves == 8 && pat_wpe_knob() == 2) return launch_pat_k<16, 8>(p, max_wg, st);
+        if (waves == 8 && pat_wpe_knob() == 4) return launch_pat_k<16, 8, 4>(p, max_wg, st);
 #endif
-        return waves == 8 ? launch_pat_k<16, 8, 4>(p, max_wg, st) : launch_pat_k<16, 4>(p, max_wg, st);
+        return waves == 8 ? launch_pat_k<16, 8>(p, max_wg, st) : launch_pat_k<16, 4>(p, max_wg, st);
     default: return launch_pat_k<32, 8>(p, max_wg, st);
     }
 }
