@@ -118,7 +118,10 @@ Split choose_split(int M, int N, int K, int precision = LRS_DIP_SPLIT_BF16, bool
         S = (int)((target + tiles - 1) / tiles);   // ~2 workgroups per CU (256 and 1024 measured slower)
         const int smax = deep ? K / 512 : (K + 127) / 128;
         if (S > smax) S = smax;
-        if (S > (deep ? 256 : 64)) S = deep ? 256 : 64;
+        // at most 64 splits otherwise (LRS_DIP_SPLIT_CAP, tuning only; 196^2 step, 2 rounds:
+        // 32 -> 1.327 ms, 64 -> 1.265, 128 -> 1.279, 256 -> 1.285; profiles/r04/split_cap/)
+        static const int cap = (int)std::max<int64_t>(1, tune_knob("LRS_DIP_SPLIT_CAP", 64));
+        if (S > (deep ? 256 : cap)) S = deep ? 256 : cap;
         if (S < 1) S = 1;
     }
     const int bk = (big && precision == LRS_DIP_SPLIT_BF16) ? kBK32 : kBK;
