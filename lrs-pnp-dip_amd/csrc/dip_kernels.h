@@ -583,6 +583,49 @@ __device__ __forceinline__ double block_sum_d(double v, double *red) {
     return s;
 }
 
+// Two / three block sums behind ONE barrier (red >= 2 / 3 x blockDim / 64 doubles): each sum is
+// formed exactly as block_sum_d1 forms it (wave sums, then the waves' values in wave order from
+// 0.0), so the results are bitwise those of consecutive block_sum_d1 calls; every thread gets them.
+__device__ __forceinline__ void block_sum2_d(double &a, double &b, double *red) {
+    const int nw = blockDim.x >> 6, w = threadIdx.x >> 6;
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    if ((threadIdx.x & 63) == 0) {
+        red[w] = a;
+        red[nw + w] = b;
+    }
+    __syncthreads();
+    double s0 = 0.0, s1 = 0.0;
+    for (int i = 0; i < nw; ++i) {
+        s0 += red[i];
+        s1 += red[nw + i];
+    }
+    a = s0;
+    b = s1;
+}
+
+__device__ __forceinline__ void block_sum3_d(double &a, double &b, double &c, double *red) {
+    const int nw = blockDim.x >> 6, w = threadIdx.x >> 6;
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    c = wave_sum_d(c);
+    if ((threadIdx.x & 63) == 0) {
+        red[w] = a;
+        red[nw + w] = b;
+        red[2 * nw + w] = c;
+    }
+    __syncthreads();
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int i = 0; i < nw; ++i) {
+        s0 += red[i];
+        s1 += red[nw + i];
+        s2 += red[2 * nw + i];
+    }
+    a = s0;
+    b = s1;
+    c = s2;
+}
+
 // ------------------------------------------------------------------------------------------
 // BatchNorm2d (train mode, batch 1) with the Lipschitz rescale, + activation.
 // Each channel is split over S workgroups (grid = S x C).  Statistics: per-workgroup fp64
@@ -603,6 +646,16 @@ __device__ float bn_lip_scale(const float *gamma, int C, float *redf) {
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r = fmaxf(r, redf[i]);
     return fmaxf(r, 1.0f);
 }
+
+// The same scale computed by every wave on its own (no barrier): the maximum of the same set of
+// |gamma|, so bitwise bn_lip_scale's value
+__device__ __forceinline__ float bn_lip_scale_w(const float *gamma, int C) {
+    float m = 0.0f;
+    for (int i = threadIdx.x & 63; i < C; i += 64) m = fmaxf(m, fabsf(gamma[i]));
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    return fmaxf(m, 1.0f);
+}
+
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
     if (act == LRS_ACT_LRELU) return v > 0.0f ? v : v * 0.2f;
@@ -629,8 +682,30 @@ struct BnArgs {
     int vec;                     // float4 path: P, chunk multiples of 4, tensors 16-B aligned
 };
 
+// The forward statistics every thread derives from the block sums (thread 0 also stores them):
+// the arithmetic k_bn_fwd1's thread 0 used, so bitwise the same mean / invstd
+__device__ __forceinline__ void bn_fwd_finish(const BnArgs &a, int c, double K, double s1, double s2, float &m32,
+                                              float &is32) {
+    const double m = s1 / a.P;
+    double var = s2 / a.P - m * m;
+    if (var < 0.0) var = 0.0;
+    m32 = (float)(K + m);
+    is32 = (float)(1.0 / sqrt(var + (double)a.eps));
+    if (threadIdx.x == 0) {
+        a.mean[c] = m32;
+        a.invstd[c] = is32;
+        if (a.run_mean) {
+            const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
+            a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
+            a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+        }
+    }
+}
+
 // partial sums of (z - K), (z - K)^2 over this workgroup's slice, K = z[c][0] (stable variance);
-// block-reduced (valid in every thread)
+// block-reduced (valid in every thread).  ONE: the whole channel in this workgroup (k_bn_fwd1): the
+// two sums behind one barrier (bitwise the same values)
+template <bool ONE = false>
 __device__ __forceinline__ void bn_stats_body(const BnArgs &a, int c, int sb, double &s1, double &s2, double *red) {
     const float *z = a.z + (int64_t)c * a.P;
     const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
@@ -654,9 +729,13 @@ __device__ __forceinline__ void bn_stats_body(const BnArgs &a, int c, int sb, do
             s2 += d * d;
         }
     }
-    int par = 0;
-    s1 = block_sum_d1(s1, red, par);
-    s2 = block_sum_d1(s2, red, par);
+    if constexpr (ONE) {
+        block_sum2_d(s1, s2, red);
+    } else {
+        int par = 0;
+        s1 = block_sum_d1(s1, red, par);
+        s2 = block_sum_d1(s2, red, par);
+    }
 }
 
 __global__ __launch_bounds__(kBnThreads) void k_bn_stats(BnArgs a) {
@@ -672,34 +751,43 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_stats(BnArgs a) {
 }
 
 // normalise + affine + activation of this workgroup's slice; t1, t2 = the channel's summed
-// partials (read by thread 0 only)
+// partials (read by thread 0 only).  ONE (k_bn_fwd1): t1, t2 valid in every thread, which then all
+// form the statistics themselves (thread 0's arithmetic) and the Lipschitz scale per wave: no barrier
+template <bool ONE = false>
 __device__ __forceinline__ void bn_apply_body(const BnArgs &a, int c, int sb, double t1, double t2, float *redf,
                                               float *st_s) {
     const int64_t off = (int64_t)c * a.P;
     const float *z = a.z + off;
     float *y = a.y + off;
     const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
-    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
-    if (threadIdx.x == 0) {
-        const double m = t1 / a.P;
-        double var = t2 / a.P - m * m;
-        if (var < 0.0) var = 0.0;
-        const float m32 = (float)((double)a.z[off] + m);
-        const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
-        st_s[0] = m32;
-        st_s[1] = is32;
-        if (sb == 0) {
-            a.mean[c] = m32;
-            a.invstd[c] = is32;
-            if (a.run_mean) {
-                const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
-                a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
-                a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+    float cs, m32, is32;
+    if constexpr (ONE) {
+        cs = a.lip ? bn_lip_scale_w(a.gamma, a.C) : 1.0f;
+        bn_fwd_finish(a, c, (double)a.z[off], t1, t2, m32, is32);
+    } else {
+        cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+        if (threadIdx.x == 0) {
+            const double m = t1 / a.P;
+            double var = t2 / a.P - m * m;
+            if (var < 0.0) var = 0.0;
+            const float m32 = (float)((double)a.z[off] + m);
+            const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
+            st_s[0] = m32;
+            st_s[1] = is32;
+            if (sb == 0) {
+                a.mean[c] = m32;
+                a.invstd[c] = is32;
+                if (a.run_mean) {
+                    const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
+                    a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
+                    a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+                }
             }
         }
+        __syncthreads();
+        m32 = st_s[0];
+        is32 = st_s[1];
     }
-    __syncthreads();
-    const float m32 = st_s[0], is32 = st_s[1];
     const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
     if (a.vec) {
         const float4 *z4 = reinterpret_cast<const float4 *>(z);
@@ -740,8 +828,8 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd1(BnArgs a) {
     __shared__ float st_s[2];
     const int c = blockIdx.y;
     double s1, s2;
-    bn_stats_body(a, c, 0, s1, s2, red);
-    bn_apply_body(a, c, 0, 0.0 + s1, 0.0 + s2, redf, st_s);
+    bn_stats_body<true>(a, c, 0, s1, s2, red);
+    bn_apply_body<true>(a, c, 0, 0.0 + s1, 0.0 + s2, redf, st_s);
 }
 
 // Split-K finish + BatchNorm(+act) of one channel in one launch (a channel fits one workgroup:
@@ -751,16 +839,9 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd1(BnArgs a) {
 __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn1(const float *__restrict__ part, int nsplit,
                                                             const float *__restrict__ bias, BnArgs a) {
     __shared__ double red[2 * kBn1Threads / 64];
-    __shared__ float redf[kBn1Threads / 64];
-    __shared__ float st_s[3];
     const int c = blockIdx.y, t = threadIdx.x;
     const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
-    float zv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int i = t + u * kBn1Threads;
-        zv[u] = 0.0f;
-        if (i >= a.P) continue;
+    auto zsum = [&](int i) {
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         int zz = 0;
         for (; zz + 8 <= nsplit; zz += 8)
@@ -769,12 +850,21 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn1(const float *__restr
         for (; zz < nsplit; ++zz) acc[zz & 7] += part[(int64_t)zz * MN + off + i];
         float v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
         if (bias) v = v + bias[c];
-        zv[u] = v;
-        const_cast<float *>(a.z)[off + i] = v;
+        return v;
+    };
+    const float cs = a.lip ? bn_lip_scale_w(a.gamma, a.C) : 1.0f;
+    float zv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = t + u * kBn1Threads;
+        zv[u] = 0.0f;
+        if (i >= a.P) continue;
+        zv[u] = zsum(i);
+        const_cast<float *>(a.z)[off + i] = zv[u];
     }
-    if (t == 0) st_s[2] = zv[0];
-    __syncthreads();
-    const double K = (double)st_s[2];
+    // K = z[c][0], formed again by every thread (the same sum, so the same value) instead of being
+    // broadcast from thread 0 behind a barrier
+    const double K = (double)zsum(0);
     double s1 = 0.0, s2 = 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -783,28 +873,9 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn1(const float *__restr
             s1 += d;
             s2 += d * d;
         }
-    int par = 0;
-    s1 = block_sum_d1(s1, red, par);
-    s2 = block_sum_d1(s2, red, par);
-    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
-    if (t == 0) {
-        const double m = s1 / a.P;
-        double var = s2 / a.P - m * m;
-        if (var < 0.0) var = 0.0;
-        const float m32 = (float)(K + m);
-        const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
-        st_s[0] = m32;
-        st_s[1] = is32;
-        a.mean[c] = m32;
-        a.invstd[c] = is32;
-        if (a.run_mean) {
-            const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
-            a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
-            a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
-        }
-    }
-    __syncthreads();
-    const float m32 = st_s[0], is32 = st_s[1];
+    block_sum2_d(s1, s2, red);   // the only barrier
+    float m32, is32;
+    bn_fwd_finish(a, c, K, s1, s2, m32, is32);
     const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -842,7 +913,9 @@ __device__ __forceinline__ float bn_act_bwd(float g, float xh, float gm, float b
 }
 
 // redf: the Lipschitz scale's reduction scratch (kBn*Threads / 64 floats); with beta the LeakyReLU
-// branch comes from the pre-activation (bn_act_bwd), so y is not read
+// branch comes from the pre-activation (bn_act_bwd), so y is not read.  ONE (k_bn_bwd1): the scale
+// per wave and the three sums behind one barrier (red >= 3 x blockDim / 64; bitwise the same values)
+template <bool ONE = false>
 __device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int sb, double (&o)[3], double *red,
                                                   float *redf) {
     const int64_t off = (int64_t)c * a.P;
@@ -852,7 +925,9 @@ __device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int
     const bool ldy = bn_needs_y(a);
     float gm = 0.0f, bt = 0.0f;
     if (a.bn && !ldy) {
-        const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+        float cs = 1.0f;
+        if constexpr (ONE) cs = a.lip ? bn_lip_scale_w(a.gamma, a.C) : 1.0f;
+        else cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
         gm = a.gamma[c] / cs;
         bt = a.beta[c] / cs;
     }
@@ -886,10 +961,17 @@ __device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int
     } else {
         for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) sg += (double)act_bwd(gy[i], y[i], a.act);
     }
-    int par = 0;
-    o[0] = block_sum_d1(sg, red, par);
-    o[1] = block_sum_d1(sgx, red, par);
-    o[2] = block_sum_d1(sx, red, par);
+    if constexpr (ONE) {
+        block_sum3_d(sg, sgx, sx, red);
+        o[0] = sg;
+        o[1] = sgx;
+        o[2] = sx;
+    } else {
+        int par = 0;
+        o[0] = block_sum_d1(sg, red, par);
+        o[1] = block_sum_d1(sgx, red, par);
+        o[2] = block_sum_d1(sx, red, par);
+    }
 }
 
 __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
@@ -906,7 +988,9 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
     }
 }
 
-// t = the channel's summed partials (read by thread 0 only)
+// t = the channel's summed partials (read by thread 0 only).  ONE (k_bn_bwd1): t valid in every
+// thread, which then all form mean(g), mean(g x_hat) themselves and the scale per wave: no barrier
+template <bool ONE = false>
 __device__ __forceinline__ void bn_bwd_apply_body(const BnBwdArgs &a, int c, int sb, const double (&t)[3],
                                                   float *redf, float *st_s) {
     const int64_t off = (int64_t)c * a.P;
@@ -921,25 +1005,34 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnBwdArgs &a, int c, int
         }
         return;
     }
-    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    float cs = 1.0f;
+    if constexpr (ONE) cs = a.lip ? bn_lip_scale_w(a.gamma, a.C) : 1.0f;
+    else cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
     const float m32 = a.mean[c], is32 = a.invstd[c];
     const float gm = a.gamma[c] / cs;
     const float k = gm * is32;
     const bool ldy = bn_needs_y(a);
     const float bt = ldy ? 0.0f : a.beta[c] / cs;
-    if (threadIdx.x == 0) {
-        const float mg = (float)(t[0] / a.P), mgx = (float)(t[1] / a.P);
-        st_s[0] = mg;
-        st_s[1] = mgx;
-        if (sb == 0) {
+    float mg, mgx;
+    if (ONE || threadIdx.x == 0) {
+        mg = (float)(t[0] / a.P);
+        mgx = (float)(t[1] / a.P);
+        if (!ONE) {
+            st_s[0] = mg;
+            st_s[1] = mgx;
+        }
+        if (threadIdx.x == 0 && sb == 0) {
             a.ggamma[c] = (float)t[1] / cs;
             a.gbeta[c] = (float)t[0] / cs;
             // conv bias grad = sum_p gz = k (sg - P mg - mgx sum_p xhat)  (zero in exact arithmetic)
             if (a.gbias) a.gbias[c] = (float)((double)k * (t[0] - (double)a.P * mg - (double)mgx * t[2]));
         }
     }
-    __syncthreads();
-    const float mg = st_s[0], mgx = st_s[1];
+    if constexpr (!ONE) {
+        __syncthreads();
+        mg = st_s[0];
+        mgx = st_s[1];
+    }
     if (a.vec) {
         const float4 *gy4 = reinterpret_cast<const float4 *>(gy), *y4 = reinterpret_cast<const float4 *>(y),
                      *z4 = reinterpret_cast<const float4 *>(z);
@@ -988,14 +1081,14 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_apply(BnBwdArgs a) {
 
 // S == 1: statistics and apply in one launch (same arithmetic as the two-kernel path)
 __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd1(BnBwdArgs a) {
-    __shared__ double red[2 * kBn1Threads / 64];
+    __shared__ double red[3 * kBn1Threads / 64];
     __shared__ float redf[kBn1Threads / 64];
     __shared__ float st_s[2];
     const int c = blockIdx.y;
     double o[3];
-    bn_bwd_stats_body(a, c, 0, o, red, redf);
+    bn_bwd_stats_body<true>(a, c, 0, o, red, redf);
     const double t[3] = {0.0 + o[0], 0.0 + o[1], 0.0 + o[2]};
-    bn_bwd_apply_body(a, c, 0, t, redf, st_s);
+    bn_bwd_apply_body<true>(a, c, 0, t, redf, st_s);
 }
 
 // ---- one workgroup per channel, the channel held in registers (P <= 4096 NQ, float4 path) ----
@@ -1046,10 +1139,9 @@ template <int NQ, int TH = kBn1Threads>
 __global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part, int nsplit,
                                                           const float *__restrict__ bias, BnArgs a) {
     __shared__ double red[2 * kBn1Threads / 64];
-    __shared__ float redf[kBn1Threads / 64];
-    __shared__ float st_s[3];
     const int c = blockIdx.y, t = threadIdx.x;
     const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
+    const float cs = a.lip ? bn_lip_scale_w(a.gamma, a.C) : 1.0f;
     float4 zv[NQ];
     float4 *z4 = reinterpret_cast<float4 *>(const_cast<float *>(a.z) + off);
 #pragma unroll
@@ -1071,9 +1163,15 @@ __global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part,
         zv[u] = v;
         z4[q] = v;
     }
-    if (t == 0) st_s[2] = zv[0].x;
-    __syncthreads();
-    const double K = (double)st_s[2];
+    // K = z[c][0] (thread 0's first value), formed again by every thread: no broadcast barrier
+    float k0;
+    if (part) {
+        k0 = splitk_sum4(part, nsplit, MN, off, 0).x;
+        if (bias) k0 = k0 + bias[c];
+    } else {
+        k0 = z4[0].x;
+    }
+    const double K = (double)k0;
     double s1 = 0.0, s2 = 0.0;
 #pragma unroll
     for (int u = 0; u < NQ; ++u)
@@ -1085,28 +1183,9 @@ __global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part,
             s1 += d2; s2 += d2 * d2;
             s1 += d3; s2 += d3 * d3;
         }
-    int par = 0;
-    s1 = block_sum_d1(s1, red, par);
-    s2 = block_sum_d1(s2, red, par);
-    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
-    if (t == 0) {
-        const double m = s1 / a.P;
-        double var = s2 / a.P - m * m;
-        if (var < 0.0) var = 0.0;
-        const float m32 = (float)(K + m);
-        const float is32 = (float)(1.0 / sqrt(var + (double)a.eps));
-        st_s[0] = m32;
-        st_s[1] = is32;
-        a.mean[c] = m32;
-        a.invstd[c] = is32;
-        if (a.run_mean) {
-            const double unb = a.P > 1 ? var * a.P / (a.P - 1) : var;
-            a.run_mean[c] = (1.0f - a.momentum) * a.run_mean[c] + a.momentum * m32;
-            a.run_var[c] = (1.0f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
-        }
-    }
-    __syncthreads();
-    const float m32 = st_s[0], is32 = st_s[1];
+    block_sum2_d(s1, s2, red);   // the only barrier
+    float m32, is32;
+    bn_fwd_finish(a, c, K, s1, s2, m32, is32);
     const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
     float4 *y4 = reinterpret_cast<float4 *>(a.y + off);
 #pragma unroll
@@ -1125,13 +1204,11 @@ __global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part,
 // Replaces k_gemm_reduce + k_bn_bwd1 below a small-map conv's data gradient.
 __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__restrict__ part, int nsplit,
                                                                 BnBwdArgs a) {
-    __shared__ double red[2 * kBn1Threads / 64];
-    __shared__ float redf[kBn1Threads / 64];
-    __shared__ float st_s[2];
+    __shared__ double red[3 * kBn1Threads / 64];
     const int c = blockIdx.y, t = threadIdx.x;
     const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
     const float m32 = a.mean[c], is32 = a.invstd[c];
-    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    const float cs = a.lip ? bn_lip_scale_w(a.gamma, a.C) : 1.0f;
     const float gm = a.gamma[c] / cs, bt = a.beta ? a.beta[c] / cs : 0.0f;
     const bool ldy = bn_needs_y(a);
     float g[4], xh[4];
@@ -1157,21 +1234,14 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__r
         sgx += (double)g[u] * (double)xh[u];
         sx += (double)xh[u];
     }
-    int par = 0;
-    sg = block_sum_d1(sg, red, par);
-    sgx = block_sum_d1(sgx, red, par);
-    sx = block_sum_d1(sx, red, par);
+    block_sum3_d(sg, sgx, sx, red);   // the only barrier
     const float k = gm * is32;
+    const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
     if (t == 0) {
-        const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
-        st_s[0] = mg;
-        st_s[1] = mgx;
         a.ggamma[c] = (float)sgx / cs;
         a.gbeta[c] = (float)sg / cs;
         if (a.gbias) a.gbias[c] = (float)((double)k * (sg - (double)a.P * mg - (double)mgx * sx));
     }
-    __syncthreads();
-    const float mg = st_s[0], mgx = st_s[1];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = t + u * kBn1Threads;
@@ -1185,15 +1255,13 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__r
 // dL/dz = k (g - mean(g) - x_hat mean(g x_hat)) (+= when accumulating), and the parameter grads
 template <int NQ>
 __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd_r(BnBwdArgs a) {
-    __shared__ double red[2 * kBn1Threads / 64];
-    __shared__ float redf[kBn1Threads / 64];
-    __shared__ float st_s[2];
+    __shared__ double red[3 * kBn1Threads / 64];
     const int c = blockIdx.y, t = threadIdx.x;
     const int64_t off = (int64_t)c * a.P;
     const float4 *gy4 = reinterpret_cast<const float4 *>(a.gy + off), *y4 = reinterpret_cast<const float4 *>(a.y + off),
                  *z4 = reinterpret_cast<const float4 *>(a.z + off);
     const float m32 = a.mean[c], is32 = a.invstd[c];
-    const float cs = a.lip ? bn_lip_scale(a.gamma, a.C, redf) : 1.0f;
+    const float cs = a.lip ? bn_lip_scale_w(a.gamma, a.C) : 1.0f;
     const float gm = a.gamma[c] / cs, bt = a.beta ? a.beta[c] / cs : 0.0f;
     const bool ldy = bn_needs_y(a);
     float g[NQ][4], xh[NQ][4];
@@ -1215,21 +1283,14 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_bwd_r(BnBwdArgs a) {
             sx += (double)xh[u][e];
         }
     }
-    int par = 0;
-    sg = block_sum_d1(sg, red, par);
-    sgx = block_sum_d1(sgx, red, par);
-    sx = block_sum_d1(sx, red, par);
+    block_sum3_d(sg, sgx, sx, red);   // the only barrier
     const float k = gm * is32;
+    const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
     if (t == 0) {
-        const float mg = (float)(sg / a.P), mgx = (float)(sgx / a.P);
-        st_s[0] = mg;
-        st_s[1] = mgx;
         a.ggamma[c] = (float)sgx / cs;
         a.gbeta[c] = (float)sg / cs;
         if (a.gbias) a.gbias[c] = (float)((double)k * (sg - (double)a.P * mg - (double)mgx * sx));
     }
-    __syncthreads();
-    const float mg = st_s[0], mgx = st_s[1];
     float4 *gz4 = reinterpret_cast<float4 *>(a.gz + off);
 #pragma unroll
     for (int u = 0; u < NQ; ++u)
