@@ -703,9 +703,7 @@ __device__ __forceinline__ void bn_fwd_finish(const BnArgs &a, int c, double K, 
 }
 
 // partial sums of (z - K), (z - K)^2 over this workgroup's slice, K = z[c][0] (stable variance);
-// block-reduced (valid in every thread).  ONE: the whole channel in this workgroup (k_bn_fwd1): the
-// two sums behind one barrier (bitwise the same values)
-template <bool ONE = false>
+// block-reduced (valid in every thread), both sums behind one barrier
 __device__ __forceinline__ void bn_stats_body(const BnArgs &a, int c, int sb, double &s1, double &s2, double *red) {
     const float *z = a.z + (int64_t)c * a.P;
     const int i0 = sb * a.chunk, i1 = min(a.P, i0 + a.chunk);
@@ -729,13 +727,7 @@ __device__ __forceinline__ void bn_stats_body(const BnArgs &a, int c, int sb, do
             s2 += d * d;
         }
     }
-    if constexpr (ONE) {
-        block_sum2_d(s1, s2, red);
-    } else {
-        int par = 0;
-        s1 = block_sum_d1(s1, red, par);
-        s2 = block_sum_d1(s2, red, par);
-    }
+    block_sum2_d(s1, s2, red);
 }
 
 __global__ __launch_bounds__(kBnThreads) void k_bn_stats(BnArgs a) {
@@ -828,7 +820,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd1(BnArgs a) {
     __shared__ float st_s[2];
     const int c = blockIdx.y;
     double s1, s2;
-    bn_stats_body<true>(a, c, 0, s1, s2, red);
+    bn_stats_body(a, c, 0, s1, s2, red);
     bn_apply_body<true>(a, c, 0, 0.0 + s1, 0.0 + s2, redf, st_s);
 }
 
@@ -913,8 +905,8 @@ __device__ __forceinline__ float bn_act_bwd(float g, float xh, float gm, float b
 }
 
 // redf: the Lipschitz scale's reduction scratch (kBn*Threads / 64 floats); with beta the LeakyReLU
-// branch comes from the pre-activation (bn_act_bwd), so y is not read.  ONE (k_bn_bwd1): the scale
-// per wave and the three sums behind one barrier (red >= 3 x blockDim / 64; bitwise the same values)
+// branch comes from the pre-activation (bn_act_bwd), so y is not read.  The three sums behind one
+// barrier (red >= 3 x blockDim / 64 doubles); ONE (k_bn_bwd1): the scale per wave (no barrier)
 template <bool ONE = false>
 __device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int sb, double (&o)[3], double *red,
                                                   float *redf) {
@@ -961,21 +953,14 @@ __device__ __forceinline__ void bn_bwd_stats_body(const BnBwdArgs &a, int c, int
     } else {
         for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) sg += (double)act_bwd(gy[i], y[i], a.act);
     }
-    if constexpr (ONE) {
-        block_sum3_d(sg, sgx, sx, red);
-        o[0] = sg;
-        o[1] = sgx;
-        o[2] = sx;
-    } else {
-        int par = 0;
-        o[0] = block_sum_d1(sg, red, par);
-        o[1] = block_sum_d1(sgx, red, par);
-        o[2] = block_sum_d1(sx, red, par);
-    }
+    block_sum3_d(sg, sgx, sx, red);
+    o[0] = sg;
+    o[1] = sgx;
+    o[2] = sx;
 }
 
 __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_stats(BnBwdArgs a) {
-    __shared__ double red[2 * kBnThreads / 64];
+    __shared__ double red[3 * kBnThreads / 64];
     __shared__ float redf[kBnThreads / 64];
     const int c = blockIdx.y, sb = blockIdx.x;
     double o[3];
@@ -1862,8 +1847,7 @@ __global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out,
         }
     }
     int parity = 0;
-    s = block_sum_d1(s, red, parity);
-    sb = block_sum_d1(sb, red, parity);
+    block_sum2_d(s, sb, red);   // (red is free again after the barrier below)
     double *bp = part + (int64_t)c * S, *lp = part + (int64_t)C * S + (int64_t)c * S;
     double *cl = part + 2 * (int64_t)C * S;   // per-channel losses
     // hand-offs without fences (lrs_common.h, wt_store): write-through partials, drain, count
@@ -1878,8 +1862,7 @@ __global__ __launch_bounds__(256) void k_mse_head(const float *__restrict__ out,
     // the channel's partials, summed by the whole workgroup in a fixed tree (S <= 64): deterministic
     const int t = threadIdx.x;
     double tb = t < S ? wt_load(bp + t) : 0.0, tl = t < S ? wt_load(lp + t) : 0.0;
-    tb = block_sum_d1(tb, red, parity);
-    tl = block_sum_d1(tl, red, parity);
+    block_sum2_d(tb, tl, red);
     if (t == 0) {
         gbias[c] = (float)tb;
         agent_store(cnt + c, 0);
