@@ -495,10 +495,13 @@ inline bool conv_implicit_ok(const ConvGeom &g, int Cout) {
 
 // The engine runs a conv as an implicit GEMM from this many output pixels up; below it the maps
 // are small enough that an explicit im2col into a cached col buffer plus the 64-tile GEMMs is
-// faster (measured at 36x36: 1.23 vs 1.41 ms per U-Net step).  LRS_DIP_IMPLICIT_MIN_P overrides
-// (tuning only).
+// faster (round 1, at 36x36: 1.23 vs 1.41 ms per U-Net step).  Round 4 re-measured the kernels of
+// today: 2048 -> 1024 moves the 36^2 maps (1296 pixels) to the implicit paths, 36^2 step 0.652 ->
+// 0.638 ms, and the skip net's 32^2 maps, 512^2 step 9.27 -> 9.23 ms; 512 (the 196^2 net's 25^2 maps
+// too) is slower there, 1.244 -> 1.288 ms (profiles/r04/implicit_min_p/).
+// LRS_DIP_IMPLICIT_MIN_P overrides (tuning only).
 inline int64_t implicit_min_pixels() {
-    static const int64_t v = tune_knob("LRS_DIP_IMPLICIT_MIN_P", 2048);
+    static const int64_t v = tune_knob("LRS_DIP_IMPLICIT_MIN_P", 1024);
     return v;
 }
 
