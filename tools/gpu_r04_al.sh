@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 4: the DIP engine's launch knobs re-swept at the native 36^2 size on the current kernels
+# (tuning build), 2 interleaved rounds, each config against the default of its round.
+set -o pipefail
+o=gpurun_out/r04al
+mkdir -p $o
+export TMPDIR=/tmp
+T=$PWD/lrs-pnp-dip_amd/lrspnp/liblrspnp_hip_tune.so
+run() {
+  env LRSPNP_LIB=$T "$@" timeout -k 10 200 python tools/dip_steptime.py --net unet --hw 36 --bands 128 --rounds 3 > $o/st.txt 2>&1 || { tail $o/st.txt; return 1; }
+  echo "$* : $(tail -1 $o/st.txt)"
+}
+for r in 1 2; do
+  run X=default || exit 1
+  run LRS_DIP_UPC=0 || exit 1
+  run LRS_DIP_SM_WG=320 || exit 1
+  run LRS_DIP_SM_WG=1280 || exit 1
+  run LRS_DIP_PREP_WG=256 || exit 1
+  run LRS_DIP_FWD_SPLIT_WG=256 || exit 1
+  run LRS_DIP_FWD_SPLIT_WG=512 || exit 1
+  run LRS_DIP_DGRAD_SPLIT_WG=256 || exit 1
+  run LRS_DIP_SPLIT_CAP=32 || exit 1
+done
