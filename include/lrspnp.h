@@ -381,8 +381,8 @@ const float *lrs_dipnet_node_buffer(const lrs_dipnet *net, int node, int which);
 /* nsteps training steps: forward, masked MSE, backward, Adam; es (nullable) gets every step's
  * forward output (ring: es->size * C*H*W floats).  use_graph != 0 captures one step into a
  * hipGraph (on first use, re-captured when any argument changes) and replays it.  The weight
- * gradients run on a second stream the net owns, created with the calling stream's priority and
- * re-created when a call comes on a stream of another priority. */
+ * gradients run on a second stream the net owns with the calling stream's priority (one such
+ * stream per priority seen, kept for the net's lifetime: switching priorities costs nothing). */
 int lrs_dipnet_train_steps(lrs_dipnet *net, const float *x, const float *target, const float *mask,
                            float lr, float beta1, float beta2, float eps, lrs_es_state *es,
                            float *ring, int nsteps, int use_graph, void *stream);

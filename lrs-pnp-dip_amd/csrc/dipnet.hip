@@ -544,15 +544,9 @@ int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, 
     if (M <= 0 || N <= 0) return LRS_OK;
     if (M > 256 || lda < K || lda % 16) return LRS_E_UNSUPPORTED;
     const int Kp32 = (int)round_up(lda, 32), ldsrow = pw_ldsrow(Kp32);
-    static bool attr_set = false;
-    if (!attr_set) {   // up to K = 256: 3 x 80 x 528 B
-        const int mx = 3 * 80 * pw_ldsrow(256);
-        for (const PwKernel &k : kPwKernels) {
-            const hipError_t e = hipFuncSetAttribute((const void *)k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-            if (e != hipSuccess) return (int)e;
-        }
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> attr_set[sizeof(kPwKernels) / sizeof(kPwKernels[0])];   // per device
+    for (size_t i = 0; i < sizeof(kPwKernels) / sizeof(kPwKernels[0]); ++i)   // up to K = 256: 3 x 80 x 528 B
+        if (const int rc = lds_opt_in((const void *)kPwKernels[i].fn, 3 * 80 * pw_ldsrow(256), attr_set[i])) return rc;
     if (Kp32 > 256 || (int64_t)K * N * 4 >= kOob || 3 * pstride * 2 >= kOob) return LRS_E_UNSUPPORTED;
     static const int dbg = (int)tune_knob("LRS_PW_DBG", 0);
     const PwArgs a{A, pstride, lda, B, K, N, C, bias, M, Kp32, ldsrow, accum, dbg, act};
@@ -1145,8 +1139,8 @@ struct lrs_dipnet {
     hipGraph_t graph = nullptr;
     // weight gradients run on a side stream beside the data-gradient chain (fork per conv node
     // after its BN backward, join before Adam)
-    hipStream_t side = nullptr;
-    int side_prio = 0;   // the priority side was created with (the calling stream's)
+    hipStream_t side = nullptr;   // the one for the current call's priority (one of sides)
+    std::vector<std::pair<int, hipStream_t>> sides;   // (priority, stream): one per priority seen
     std::vector<hipEvent_t> ev_fork;
     hipEvent_t ev_join = nullptr;
     int64_t part2_off = 0;
@@ -1740,11 +1734,11 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
 extern "C" void lrs_dipnet_destroy(lrs_dipnet *net) {
     if (!net) return;
     drop_graph(net);
-    if (net->side) (void)hipStreamSynchronize(net->side);
+    for (auto &ps : net->sides) (void)hipStreamSynchronize(ps.second);
     for (hipEvent_t ev : net->ev_fork)
         if (ev) (void)hipEventDestroy(ev);
     if (net->ev_join) (void)hipEventDestroy(net->ev_join);
-    if (net->side) (void)hipStreamDestroy(net->side);
+    for (auto &ps : net->sides) (void)hipStreamDestroy(ps.second);
     delete net;
 }
 
@@ -1901,33 +1895,31 @@ extern "C" const float *lrs_dipnet_node_buffer(const lrs_dipnet *net, int node, 
     return off >= 0 ? net->f(off) : nullptr;
 }
 
-// The side stream and its fork/join events are created on the first training call (outside any
-// capture), so that creating a net and querying its layout needs no device.
+// The side streams and the fork/join events are created on the first training call that needs
+// them (outside any capture), so that creating a net and querying its layout needs no device.
 // The side stream takes the priority of the calling stream, so a caller that trains the net on a
 // high-priority stream (LrsPnPConfig.lowrank_priority) gets its weight gradients placed with the
-// same priority; a call on a stream of another priority re-creates it (after the old one drains;
-// a captured graph that names it is dropped).
+// same priority.  One side stream is kept per priority seen (at most two in practice), so a call
+// on a stream of another priority only selects a different one: no host synchronisation and no
+// graph drop (a captured graph holds its own nodes, not the stream).
 static int ensure_side(lrs_dipnet *net, hipStream_t st) {
     if (!net->fork_w) return LRS_OK;
     int prio = 0;
     hipError_t e = hipStreamGetPriority(st, &prio);
     if (e != hipSuccess) return (int)e;
-    if (net->side) {
-        if (prio == net->side_prio) return LRS_OK;
-        drop_graph(net);
-        e = hipStreamSynchronize(net->side);
-        if (e == hipSuccess) e = hipStreamDestroy(net->side);
-        net->side = nullptr;
-        if (e != hipSuccess) return (int)e;
-        e = hipStreamCreateWithPriority(&net->side, hipStreamNonBlocking, prio);
-        if (e == hipSuccess) net->side_prio = prio;
-        return (int)e;
-    }
-    e = hipStreamCreateWithPriority(&net->side, hipStreamNonBlocking, prio);
-    if (e == hipSuccess) net->side_prio = prio;
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming);
+    for (auto &ps : net->sides)
+        if (ps.first == prio) {
+            net->side = ps.second;
+            return LRS_OK;
+        }
+    hipStream_t s = nullptr;
+    e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio);
+    if (e != hipSuccess) return (int)e;
+    net->sides.emplace_back(prio, s);
+    net->side = s;
+    if (!net->ev_join) e = hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming);
     for (size_t i = 0; i < net->ev_fork.size() && e == hipSuccess; ++i)
-        e = hipEventCreateWithFlags(&net->ev_fork[i], hipEventDisableTiming);
+        if (!net->ev_fork[i]) e = hipEventCreateWithFlags(&net->ev_fork[i], hipEventDisableTiming);
     return (int)e;
 }
 

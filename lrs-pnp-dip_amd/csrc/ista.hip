@@ -1173,9 +1173,14 @@ __global__ __launch_bounds__(kB3Threads, 1) void k_ista_ln2(IstaParams p) {
 // A second instantiation of k_ista_ln2 (the DIV = 0 quotient, never launched) beside the product's
 // <256, false, 1, true, 1>: with it the product kernel compiles to exactly round 1's code (30 AGPRs,
 // 104 v_accvgpr moves); compiled alone, the same source gets 82 AGPRs and 241 moves, and configs[1]
-// loses 2.8 % (k_ista_ln2 7.88 vs 7.59 ms per launch; profiles/r04/ab_pnp).  LLVM's inlining of the
-// shared helpers depends on how many kernels call them, and with it the register allocation of this
-// VGPR-saturated kernel.
+// loses 2.8 % (k_ista_ln2 7.88 vs 7.59 ms per launch; profiles/r04/ab_pnp).  Every helper is
+// __forceinline__, so this is not inlining: the device IR of the product kernel differs in what the
+// middle end leaves to the backend (with the second instantiation a dozen [4 x float] / <4 x float>
+// allocas survive to AMDGPUPromoteAlloca; alone, SROA splits them earlier), and the register
+// allocation of this VGPR-saturated kernel follows.  amdgpu_waves_per_eu, amdgpu_num_vgpr and
+// amdgpu_flat_work_group_size on the kernel leave 82.  tests/test_codegen.py reads the built
+// library's kernel metadata and fails above 32 AGPRs (or on any spill), so a compiler update or an
+// edit here that loses the allocation is caught on the CPU.
 template __global__ void k_ista_ln2<256, false, 1, true, 0>(IstaParams);
 
 // Standalone NLM over nvec columns of length K (any K >= 1): one workgroup per column, the
@@ -1213,16 +1218,11 @@ __global__ __launch_bounds__(256) void k_nlm_col(const float *__restrict__ g, in
 }
 
 // k_nlm_col's dynamic LDS is (K + 10) floats: above 64 KiB (K > 16374) the launch must be opted into
-// more (gfx950: 160 KiB per workgroup).  Set once per process.
+// more (gfx950: 160 KiB per workgroup).  Set once per device.
 static int nlm_col_lds(int64_t K) {
     const size_t bytes = (size_t)(K + 10) * sizeof(float);
-    static bool opted = false;
-    if (bytes > 65536 && !opted) {
-        const hipError_t e = hipFuncSetAttribute((const void *)k_nlm_col, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 160 * 1024);
-        if (e != hipSuccess) return (int)e;
-        opted = true;
-    }
+    static std::atomic<uint64_t> opted{0};
+    if (bytes > 65536) return lds_opt_in((const void *)k_nlm_col, 160 * 1024, opted);
     return LRS_OK;
 }
 

@@ -167,11 +167,12 @@ __global__ __launch_bounds__(64 * S, WPE) void k_ista_pat(IstaPatParams p) {
     }
     for (int64_t tile = first; tile < p.ntiles; tile += gridDim.x) {
         if (tile != first) __syncthreads();   // the previous tile's last reads of xbuf / gbuf are done
-        // tile descriptor (clamped: a malformed plan cannot address outside the arrays)
+        // tile descriptor (clamped: a malformed plan cannot address outside the arrays; a start
+        // outside [0, nb) makes the tile empty)
         const int64_t start = tiles[2 * tile];
         const int pc = tiles[2 * tile + 1];
         const int pat = (int)std::min<int64_t>(std::max(pc >> 5, 0), p.npat - 1);
-        const int cnt = std::min(pc & 31, 16);
+        const int cnt = (start >= 0 && start < p.nb) ? std::min(pc & 31, 16) : 0;
         const int64_t jo = start + jl;
         int64_t j = (jl < cnt && jo < p.nb) ? order[jo] : -1;
         const bool valid = j >= 0 && j < p.nb;
@@ -322,8 +323,9 @@ __global__ __launch_bounds__(64 * S, WPE) void k_ista_pat(IstaPatParams p) {
 
 // ---- host side --------------------------------------------------------------------------------
 
-static int64_t pat_images_floats(int64_t n, int64_t K, int64_t npat) {
-    const int64_t NT = round_up(n, 16) / 16, NQ = pat_nq(K);
+// n_pad: the images' row count (the kernels index them with NT = n_pad / 16)
+static int64_t pat_images_floats(int64_t n_pad, int64_t K, int64_t npat) {
+    const int64_t NT = round_up(n_pad, 16) / 16, NQ = pat_nq(K);
     return 2 * NT * NQ * 64 * 4 + npat * NQ * NQ * 256;
 }
 
@@ -347,13 +349,8 @@ static int pat_wpe_knob() {   // LRS_ISTA_PAT_WPE=4: the 128-register form (two 
 
 template <int NQ, int S, int WPE = 2>
 static int launch_pat_k(const IstaPatParams &p, int64_t max_wg, hipStream_t st) {
-    static bool lds_opt_in = false;
-    if (!lds_opt_in) {
-        const hipError_t e = hipFuncSetAttribute((const void *)k_ista_pat<NQ, S, WPE>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return (int)e;
-        lds_opt_in = true;
-    }
+    static std::atomic<uint64_t> opted{0};   // per device
+    if (const int rc = lds_opt_in((const void *)k_ista_pat<NQ, S, WPE>, 160 * 1024, opted)) return rc;
     int64_t grid = p.ntiles;
     if (max_wg > 0 && grid > max_wg) grid = max_wg;
     hipLaunchKernelGGL((k_ista_pat<NQ, S, WPE>), dim3((unsigned)grid), dim3(64 * S), pat_lds_bytes(NQ), st, p);
@@ -366,7 +363,9 @@ static int launch_pat_k(const IstaPatParams &p, int64_t max_wg, hipStream_t st) 
 int ista_pat_prepare(const float *D, int64_t n, int64_t K, const uint8_t *obs_pat, int64_t npat, int64_t n_pad,
                      void *ws, size_t ws_bytes, hipStream_t st) {
     if (K < 1 || K > 512) return LRS_E_UNSUPPORTED;
-    if (!ws || ws_bytes < ista_pat_workspace(n, K, npat)) return LRS_E_WORKSPACE;
+    // sized from n_pad, which sets the images' row count (lrs_ista_pat_workspace(n) covers the
+    // n_pad = round_up(n, 16) every caller of the solver uses; a larger n_pad needs its own size)
+    if (!ws || ws_bytes < (size_t)pat_images_floats(n_pad, K, npat) * sizeof(float)) return LRS_E_WORKSPACE;
     const int NQ = pat_nq(K);
     const int NT = (int)(n_pad / 16);
     if ((int64_t)NT * NQ * 1024 >= ((int64_t)1 << 31)) return LRS_E_UNSUPPORTED;   // 32-bit buffer offsets
@@ -388,7 +387,7 @@ int ista_pat_launch(const float *Yb, const uint8_t *obs_pat, int64_t npat, const
                     int prox, float *coefs, float *phi, void *ws, size_t ws_bytes, int64_t max_wg, hipStream_t st,
                     const float *x0) {
     if (K < 1 || K > 512) return LRS_E_UNSUPPORTED;
-    if (!ws || ws_bytes < ista_pat_workspace(n, K, npat)) return LRS_E_WORKSPACE;
+    if (!ws || ws_bytes < (size_t)pat_images_floats(n_pad, K, npat) * sizeof(float)) return LRS_E_WORKSPACE;
     const int NQ = pat_nq(K);
     const int NT = (int)(n_pad / 16);
     if ((int64_t)NT * NQ * 1024 >= ((int64_t)1 << 31)) return LRS_E_UNSUPPORTED;

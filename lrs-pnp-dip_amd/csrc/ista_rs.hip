@@ -390,13 +390,8 @@ template <int NQ, int MINW, int S>
 static int launch_rs_k(const IstaRsParams &p, int64_t max_wg, hipStream_t st) {
     int64_t tiles = (p.nb + 15) / 16;
     if (max_wg > 0 && tiles > max_wg) tiles = max_wg;
-    static bool lds_opt_in = false;   // dynamic LDS beyond 64 KiB
-    if (!lds_opt_in) {
-        const hipError_t e = hipFuncSetAttribute((const void *)k_ista_rs<NQ, MINW, S>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return (int)e;
-        lds_opt_in = true;
-    }
+    static std::atomic<uint64_t> opted{0};   // dynamic LDS beyond 64 KiB, per device
+    if (const int rc = lds_opt_in((const void *)k_ista_rs<NQ, MINW, S>, 160 * 1024, opted)) return rc;
     size_t lds = rs_lds_bytes(NQ, S);
 #ifdef LRS_TUNING
     // A/B only: LRS_ISTA_RS_LDS = dynamic LDS per workgroup (bytes, >= the kernel's), e.g. 98304 holds
@@ -436,7 +431,9 @@ int ista_rs_launch(const float *Yb, const uint8_t *obs, const float *D, int64_t 
     const int NT = (int)(n_pad / 16);
     // the dictionary images are addressed by 32-bit buffer offsets (t * NQ + k) * 1024
     if ((int64_t)NT * NQ * 1024 >= ((int64_t)1 << 31)) return LRS_E_UNSUPPORTED;
-    if (!ws || ws_bytes < ista_rs_workspace(n, K)) return LRS_E_WORKSPACE;
+    // the images have NT = n_pad / 16 row tiles: size the check from n_pad (ista_rs_workspace(n)
+    // covers n_pad = round_up(n, 16); a larger n_pad needs lrs_ista_workspace(n_pad, ...))
+    if (!ws || ws_bytes < ista_rs_workspace(n_pad, K)) return LRS_E_WORKSPACE;
     float4 *DAf = reinterpret_cast<float4 *>(ws);
     float4 *DTf = DAf + (size_t)NT * NQ * 64;
     {

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/lrspnp.h"
 
 namespace lrs {
@@ -15,6 +17,20 @@ constexpr int kWave = 64;
 // holds C[4*(l>>4) + i][l&15], i = 0..3 (cdna_hip_programming.md §3).
 __device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) applies per device: set it once per device a
+// kernel is launched on (bit d of `done` = device d done; devices >= 64 are set on every call).
+inline int lds_opt_in(const void *fn, int bytes, std::atomic<uint64_t> &done) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    const uint64_t bit = dev < 64 ? (uint64_t)1 << dev : 0;
+    if (bit && (done.load(std::memory_order_relaxed) & bit)) return 0;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return (int)e;
+    done.fetch_or(bit, std::memory_order_relaxed);
+    return 0;
 }
 
 __host__ __device__ constexpr int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }

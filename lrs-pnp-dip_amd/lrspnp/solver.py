@@ -162,6 +162,11 @@ class LrsPnP:
         self.pat_plan = None
         if cfg.ista_patterns not in ("auto", "on", "off"):
             raise LrsError(f"unknown ista_patterns {cfg.ista_patterns!r} (auto | on | off)")
+        # every mode string is checked here, before anything is enqueued (not halfway through step())
+        if cfg.ista_dip_order not in ("beside", "before"):
+            raise LrsError(f"unknown ista_dip_order {cfg.ista_dip_order!r} (beside | before)")
+        if cfg.svt_multi_wg not in ("auto", "on", "off"):
+            raise LrsError(f"unknown svt_multi_wg {cfg.svt_multi_wg!r} (auto | on | off)")
         if self.K <= 512 and (cfg.ista_patterns == "on" or (
                 cfg.ista_patterns == "auto" and ops.ista_pat_preferred(n, self.K, self.nb, self.npat, cfg.Nit))):
             plan, self.pat_ntiles = ops.ista_pat_plan(inv.reshape(-1), self.npat)

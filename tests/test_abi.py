@@ -115,3 +115,24 @@ def test_ista_pattern_cost_model():
     assert not ops.ista_pat_preferred(1296, 256, 6408, 6408, 100)
     assert not ops.ista_pat_preferred(64, 256, 125000, 40, 80)
     assert not ops.ista_pat_preferred(1296, 768, 6408, 27, 100)   # K > 512: the generic path
+
+
+def test_workspace_sized_from_n_pad():
+    """the sparse-coding images have n_pad / 16 row tiles, so a caller passing
+    n_pad > round_up(n, 16) with the workspace sized for n is refused before anything is launched
+    (host-side check: these calls never reach the device)."""
+    L = _lib.lib()
+    n, K, npat, nb = 1296, 256, 3, 48
+    n_pad = (n + 15) // 16 * 16 + 16
+    fake = ctypes.c_void_p(4096)   # never dereferenced: the size check comes first
+    ws = L.lrs_ista_pat_workspace(n, K, npat)
+    assert ws > 0
+    assert L.lrs_ista_pat_prepare(fake, n, K, fake, npat, n_pad, fake, ws, None) == -3
+    assert L.lrs_ista_pat_f32(fake, fake, npat, fake, 3, n, n_pad, K, nb, fake, fake, 10, 0, fake, fake, None,
+                              fake, ws, None) == -3
+    wr = L.lrs_ista_workspace(n, K, 0, None)
+    assert wr > 0
+    assert L.lrs_ista_f32(fake, fake, fake, n, n_pad, K, nb, fake, fake, 10, 0, fake, fake, None, fake, wr,
+                          None) == -3
+    # sized from n_pad instead, the same calls pass the check (then need a device: not called here)
+    assert L.lrs_ista_pat_workspace(n_pad, K, npat) > ws and L.lrs_ista_workspace(n_pad, K, 0, None) > wr

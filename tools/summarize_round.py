@@ -1,6 +1,6 @@
 """Summarise tools/profile_r02.sh output into committed evidence (profiles/r02/).
 
-    python tools/summarize_r02.py gpurun_out/profile_r02 profiles/r02
+    python tools/summarize_round.py gpurun_out/<run>/profile profiles/<round>  (tools/gpu.sh profile)
 
 Per workload <wl> in {dip, pnp} (whatever was profiled):
   <wl>_kernel_stats.csv   rocprofv3 --stats of the bench command (copied)
@@ -110,5 +110,5 @@ if os.path.exists(tp):
     old = json.load(open(tp))
 old.update(traffic)
 old["correction"] = "2 x FETCH_SIZE + WRITE_SIZE per kernel (gfx950: FETCH_SIZE counts 64 B per 128-B read request)"
-old["source"] = f"{dst}/<workload>_summary.json (rocprofv3 --pmc passes of the bench command, tools/profile_r02.sh)"
+old["source"] = f"{dst}/<workload>_summary.json (rocprofv3 --pmc passes of the bench command, tools/gpu.sh profile)"
 json.dump(old, open(tp, "w"), indent=1)
