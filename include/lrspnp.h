@@ -195,8 +195,10 @@ typedef struct {
  *     and back-transformation phases spread over many workgroups (bit-identical result); for a
  *     caller whose eigensolver is on the critical path (a row-slab shard), not beside a
  *     chip-filling sparse-coding kernel.
- * s_out (nullable, device, B doubles) receives the singular values (descending).  B <= 198 (the
- * eigensolver holds the packed fp64 Gram in one CU's LDS); LRS_E_UNSUPPORTED above. */
+ * s_out (nullable, device, B doubles) receives the singular values (descending).  B <= 256: up to
+ * 198 bands the eigensolver holds the packed fp64 Gram in its CU's LDS, above it (the 224-band
+ * cubes) the same one-workgroup chain works on the packed Gram in ws (L2-resident);
+ * LRS_E_UNSUPPORTED above 256 (main_LRS_PnP.py:112-124's np.linalg.svd takes any B). */
 #define LRS_SVT_WARM 1
 #define LRS_SVT_JACOBI 2
 #define LRS_SVT_MULTI_WG 4

@@ -23,13 +23,21 @@
 namespace lrs {
 
 constexpr int kGramSlabs = 256;
-constexpr int kApSteps = 50;   // k-steps of 4 of the SVT apply: B <= 200
+// k-steps of 4 of the SVT apply: 50 up to B = 200, 64 up to 256
+__host__ __device__ constexpr int ap_steps(int64_t B) { return B <= 200 ? 50 : 64; }
 constexpr int kJacobiThreads = 1024;
-// packed fp64 triangle of 198 x 198 = 157,608 B of LDS, plus the solver's vectors and flags: at
-// Bp = 200 the one-workgroup chain would need 164,128 B (> 160 KiB), so B <= 198 (every reference
-// cube: 198 or 128 bands; LRS_E_UNSUPPORTED above)
-constexpr int kMaxBp = 198;
+// The packed fp64 triangle of 198 x 198 = 157,608 B fits the LDS beside the solver's vectors and
+// flags (at Bp = 200 the chain would need 164,128 B > 160 KiB): up to kLdsMaxBp the one-workgroup
+// chain keeps it in LDS; above (the 224-band cubes of BASELINE configs[3]/[4]) the same chain runs
+// on the packed triangle in the workspace (L2-resident: 224^2/2 x 8 B = 200 KB), with full
+// workgroup barriers instead of LDS-only ones.  kMaxBp: every phase's register / lane layout.
+constexpr int kLdsMaxBp = 198;
+constexpr int kMaxBp = 256;
 constexpr int kMaxSweeps = 40;
+
+// Gram column blocks of 16: 13 up to B = 208 (91 tile pairs), 16 up to 256 (136)
+__host__ __device__ constexpr int gram_nt(int64_t B) { return B <= 208 ? 13 : 16; }
+__host__ __device__ constexpr int gram_npairs(int nt) { return nt * (nt + 1) / 2; }
 
 struct SvtWs {
     double *partial;  // [kGramSlabs][16x16 tile pairs][256]  Gram partials
@@ -42,7 +50,7 @@ struct SvtWs {
     double *beta;     // [Bp]      Householder scalars (tridiagonal path)
     double *F;        // [Bp][4][Bp] pivoted LU rows of T - lambda_i I (inverse iteration)
     float *E;         // [B][B]
-    float *Fp;        // [kApSteps][B][4]  I - E in the apply kernel's fragment order
+    float *Fp;        // [ap_steps(B)][B][4]  I - E in the apply kernel's fragment order
     int *state;       // [0] V valid, [1] current V buffer, [2] rounds, [3] sweeps,
                       // [4] path of the last solve (1 tridiagonal, 2 Jacobi fallback, 3 Jacobi)
     int64_t Bp;
@@ -60,7 +68,7 @@ static SvtWs svt_ws_layout(void *base, int64_t P, int64_t B) {
     };
     const size_t mat = (size_t)w.Bp * w.Bp * sizeof(double);
     w.state = (int *)take(256);
-    w.partial = (double *)take((size_t)kGramSlabs * 91 * 256 * sizeof(double));   // 91 = pairs of 13 blocks
+    w.partial = (double *)take((size_t)kGramSlabs * gram_npairs(gram_nt(B)) * 256 * sizeof(double));
     w.G = (double *)take(mat);
     w.A0 = (double *)take(mat);
     w.T = (double *)take(mat);
@@ -70,7 +78,7 @@ static SvtWs svt_ws_layout(void *base, int64_t P, int64_t B) {
     w.rot = (double *)take((size_t)kMaxSweeps * (w.Bp - 1) * (w.Bp / 2) * 2 * sizeof(double));
     w.beta = (double *)take((size_t)w.Bp * sizeof(double));
     w.F = (double *)take((size_t)4 * mat);
-    w.Fp = (float *)take((size_t)kApSteps * B * 4 * sizeof(float));
+    w.Fp = (float *)take((size_t)ap_steps(B) * B * 4 * sizeof(float));
     w.E = (float *)take((size_t)B * B * sizeof(float));
     return w;
 }
@@ -104,18 +112,21 @@ __device__ __forceinline__ void rr_pair(int r, int k, int Bp, int &p, int &q) {
 // (compile-time pair lists: one instantiation per wave).  Partials [slab][pair][16*16] are
 // reduced in fixed order, so G is deterministic.
 typedef double doublex4 __attribute__((ext_vector_type(4)));
-constexpr int kGramNt = 13, kGramPairs = kGramNt * (kGramNt + 1) / 2;   // B <= 208
-constexpr int kGramChunk = 32, kGramLd = 16 * kGramNt + 4;              // rows per LDS chunk, row stride
-constexpr int kGramBatch = 13;                                          // loads in flight per thread
+// NT column blocks (B <= 16 NT) over NW waves: 13 / 4 waves (91 pairs) up to B = 208, 16 / 8 waves
+// (136 pairs, 17 accumulators per wave) up to 256
+constexpr int kGramChunk = 32;   // rows per LDS chunk (row stride 16 NT + 4)
+constexpr int kGramBatch = 13;   // loads in flight per thread
 
+template <int NT>
 struct GramPairs {
-    int a[kGramPairs], b[kGramPairs];
+    int a[gram_npairs(NT)], b[gram_npairs(NT)];
 };
-__host__ __device__ constexpr GramPairs gram_pairs() {
-    GramPairs t{};
+template <int NT>
+__host__ __device__ constexpr GramPairs<NT> gram_pairs() {
+    GramPairs<NT> t{};
     int k = 0;
-    for (int a = 0; a < kGramNt; ++a)
-        for (int b = a; b < kGramNt; ++b) {
+    for (int a = 0; a < NT; ++a)
+        for (int b = a; b < NT; ++b) {
             t.a[k] = a;
             t.b[k] = b;
             ++k;
@@ -123,25 +134,26 @@ __host__ __device__ constexpr GramPairs gram_pairs() {
     return t;
 }
 
-template <int PI>
+template <int NT, int PI>
 struct GramPair {
-    static constexpr int a = gram_pairs().a[PI], b = gram_pairs().b[PI];
+    static constexpr int a = gram_pairs<NT>().a[PI], b = gram_pairs<NT>().b[PI];
 };
 
-template <int W, int... U>
-__device__ __forceinline__ void gram_mfmas(const double (&f)[kGramNt], doublex4 (&acc)[sizeof...(U)],
+template <int NT, int NW, int W, int... U>
+__device__ __forceinline__ void gram_mfmas(const double (&f)[NT], doublex4 (&acc)[sizeof...(U)],
                                            std::integer_sequence<int, U...>) {
-    ((acc[U] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[GramPair<W + 4 * U>::a], f[GramPair<W + 4 * U>::b], acc[U], 0,
-                                                    0, 0)),
+    ((acc[U] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[GramPair<NT, W + NW * U>::a], f[GramPair<NT, W + NW * U>::b],
+                                                    acc[U], 0, 0, 0)),
      ...);
 }
 
 // Whole workgroup body for wave W (every wave runs the same staging and barriers; the pair list,
 // the accumulators and their stores are compile-time per wave, so they stay in registers).
-template <int W>
+template <int NT, int NW, int W>
 __device__ __forceinline__ void gram_body(float *Zs, const float *__restrict__ X, const float *__restrict__ L2,
                                           float c2, int B, int64_t pbeg, int64_t pend, double *__restrict__ out) {
-    constexpr int NP = (kGramPairs - W + 3) / 4;
+    constexpr int kGramPairs = gram_npairs(NT), kGramLd = 16 * NT + 4, NTH = 64 * NW;
+    constexpr int NP = (kGramPairs - W + NW - 1) / NW;
     const int lane = threadIdx.x & 63, g = lane >> 4, jl = lane & 15;
     doublex4 acc[NP];
 #pragma unroll
@@ -150,11 +162,11 @@ __device__ __forceinline__ void gram_body(float *Zs, const float *__restrict__ X
         const int rows = (int)min<int64_t>(kGramChunk, pend - c0);
         __syncthreads();
         // rows x B elements, kGramBatch loads in flight per thread, then the LDS stores
-        for (int e0 = threadIdx.x; e0 < kGramChunk * B; e0 += 256 * kGramBatch) {
+        for (int e0 = threadIdx.x; e0 < kGramChunk * B; e0 += NTH * kGramBatch) {
             float z[kGramBatch];
 #pragma unroll
             for (int u = 0; u < kGramBatch; ++u) {
-                const int e = e0 + 256 * u, rr = e / B;
+                const int e = e0 + NTH * u, rr = e / B;
                 z[u] = 0.f;
                 if (e < kGramChunk * B && rr < rows) {
                     const int64_t o = c0 * B + e;
@@ -164,43 +176,45 @@ __device__ __forceinline__ void gram_body(float *Zs, const float *__restrict__ X
             }
 #pragma unroll
             for (int u = 0; u < kGramBatch; ++u) {
-                const int e = e0 + 256 * u, rr = e / B, c = e - rr * B;
+                const int e = e0 + NTH * u, rr = e / B, c = e - rr * B;
                 if (e < kGramChunk * B) Zs[rr * kGramLd + c] = z[u];
             }
         }
-        for (int idx = threadIdx.x; idx < kGramChunk * (kGramLd - B); idx += 256) {   // zero pad columns
+        for (int idx = threadIdx.x; idx < kGramChunk * (kGramLd - B); idx += NTH) {   // zero pad columns
             const int rr = idx / (kGramLd - B), c = B + idx % (kGramLd - B);
             Zs[rr * kGramLd + c] = 0.f;
         }
         __syncthreads();
         const int rows4 = (rows + 3) & ~3;
         for (int r = 0; r < rows4; r += 4) {
-            double f[kGramNt];
+            double f[NT];
 #pragma unroll
-            for (int c = 0; c < kGramNt; ++c) f[c] = (double)Zs[(r + g) * kGramLd + 16 * c + jl];
-            gram_mfmas<W>(f, acc, std::make_integer_sequence<int, NP>{});
+            for (int c = 0; c < NT; ++c) f[c] = (double)Zs[(r + g) * kGramLd + 16 * c + jl];
+            gram_mfmas<NT, NW, W>(f, acc, std::make_integer_sequence<int, NP>{});
         }
     }
     // C/D layout of the f64 MFMA: column l & 15, row (l >> 4) + 4 r
 #pragma unroll
     for (int u = 0; u < NP; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[(int64_t)(W + 4 * u) * 256 + (g + 4 * r) * 16 + jl] = acc[u][r];
+        for (int r = 0; r < 4; ++r) out[(int64_t)(W + NW * u) * 256 + (g + 4 * r) * 16 + jl] = acc[u][r];
 }
 
-__global__ __launch_bounds__(256, 1) void k_gram_mfma(const float *__restrict__ X, const float *__restrict__ L2,
-                                                      float c2, int64_t P, int B, int64_t rows_per_slab,
-                                                      double *__restrict__ partial) {
-    __shared__ __attribute__((aligned(16))) float Zs[kGramChunk * kGramLd];
+template <int NT, int NW, int... W>
+__device__ __forceinline__ void gram_dispatch(int wv, float *Zs, const float *X, const float *L2, float c2, int B,
+                                              int64_t pbeg, int64_t pend, double *out, std::integer_sequence<int, W...>) {
+    ((wv == W ? gram_body<NT, NW, W>(Zs, X, L2, c2, B, pbeg, pend, out) : (void)0), ...);
+}
+
+template <int NT, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_gram_mfma(const float *__restrict__ X, const float *__restrict__ L2,
+                                                          float c2, int64_t P, int B, int64_t rows_per_slab,
+                                                          double *__restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float Zs[kGramChunk * (16 * NT + 4)];
     const int sl = blockIdx.x, wv = threadIdx.x >> 6;
     const int64_t pbeg = (int64_t)sl * rows_per_slab, pend = min<int64_t>(P, pbeg + rows_per_slab);
-    double *out = partial + (int64_t)sl * kGramPairs * 256;
-    switch (wv) {
-    case 0: gram_body<0>(Zs, X, L2, c2, B, pbeg, pend, out); break;
-    case 1: gram_body<1>(Zs, X, L2, c2, B, pbeg, pend, out); break;
-    case 2: gram_body<2>(Zs, X, L2, c2, B, pbeg, pend, out); break;
-    default: gram_body<3>(Zs, X, L2, c2, B, pbeg, pend, out); break;
-    }
+    double *out = partial + (int64_t)sl * gram_npairs(NT) * 256;
+    gram_dispatch<NT, NW>(wv, Zs, X, L2, c2, B, pbeg, pend, out, std::make_integer_sequence<int, NW>{});
 }
 
 // ---- 1b. fixed-order reduction of the slab partials into the full symmetric Gram ------------
@@ -212,8 +226,8 @@ __global__ __launch_bounds__(256) void k_gram_reduce16(const double *__restrict_
     if (j < i) return;
     double s = 0.0;
     if (i < B && j < B) {
-        const int a = i >> 4, b = j >> 4, npair = kGramPairs;
-        const int pi = a * kGramNt - ((a * (a - 1)) >> 1) + (b - a);
+        const int a = i >> 4, b = j >> 4, npair = gram_npairs(nt);
+        const int pi = a * nt - ((a * (a - 1)) >> 1) + (b - a);
         const int e = (i & 15) * 16 + (j & 15);
         double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int sl = 0;
@@ -267,12 +281,20 @@ __device__ __forceinline__ double wg_reduce(double v, double *red) {
     return s;
 }
 
-// The solve on A = src (packed into LDS), eigenvalues to w.lam, rounds/sweeps to w.state[2..3].
-__device__ __noinline__ void jacobi_core(double *sm, SvtWs w, const double *src) {
+// The solve on A = src (packed into LDS, or with GA into Ag in the workspace when the triangle
+// exceeds the LDS: B > kLdsMaxBp), eigenvalues to w.lam, rounds/sweeps to w.state[2..3].
+template <bool GA>
+__device__ __forceinline__ void jac_bar() {
+    if (GA) __syncthreads();
+    else lds_barrier();
+}
+
+template <bool GA>
+__device__ __noinline__ void jacobi_core(double *sm, SvtWs w, const double *src, double *Ag = nullptr) {
     const int Bp = (int)w.Bp, half = Bp / 2;
     const int npk = Bp * (Bp + 1) / 2;
-    double *A = sm;                      // packed upper triangle
-    double *rc = A + npk, *rs = rc + half, *red = rs + half;
+    double *A = GA ? Ag : sm;            // packed upper triangle
+    double *rc = GA ? sm : A + npk, *rs = rc + half, *red = rs + half;
     int *ip = (int *)(red + 16), *iq = ip + half, *rowoff = iq + half;
     __shared__ int any_rot;
     const int tid = threadIdx.x;
@@ -288,7 +310,7 @@ __device__ __noinline__ void jacobi_core(double *sm, SvtWs w, const double *src)
     const double tol = 1e-7;    // residual a_pq perturbs E = f(A) by ~|a_pq| f'(lambda): << 1e-8 relative in U
     while (sweeps < kMaxSweeps) {
         if (tid == 0) any_rot = 0;
-        lds_barrier();
+        jac_bar<GA>();
         for (int r = 0; r < Bp - 1; ++r) {
             if (tid < half) {
                 int p, q;
@@ -310,7 +332,7 @@ __device__ __noinline__ void jacobi_core(double *sm, SvtWs w, const double *src)
                 log[0] = c;
                 log[1] = s;
             }
-            lds_barrier();
+            jac_bar<GA>();
             // A <- J^T A J on every unordered 2x2 block (k1 <= k2); J = [[c, s], [-s, c]] on (p, q).
             // One wave per k1 (wave-uniform rotation), lanes over k2; identity pairs are skipped.
             for (int k1 = wv; k1 < half; k1 += kJacobiThreads / 64) {
@@ -345,12 +367,12 @@ __device__ __noinline__ void jacobi_core(double *sm, SvtWs w, const double *src)
                     }
                 }
             }
-            lds_barrier();
+            jac_bar<GA>();
             ++rounds;
         }
         ++sweeps;
         const int rotated = any_rot;
-        lds_barrier();   // every thread has read the flag before thread 0 resets it
+        jac_bar<GA>();   // every thread has read the flag before thread 0 resets it
         if (!rotated) break;
     }
     for (int i = tid; i < Bp; i += kJacobiThreads) w.lam[i] = A[rowoff[i] + i];
@@ -361,10 +383,12 @@ __device__ __noinline__ void jacobi_core(double *sm, SvtWs w, const double *src)
     __syncthreads();   // rotation log and eigenvalues visible to the workgroup (in-kernel fallback)
 }
 
+// GA: the triangle in w.T (free here: the warm start's G V product is consumed into A0)
+template <bool GA>
 __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm) {
     extern __shared__ double sm[];
     const bool use_warm = warm && w.state[0] == 1;
-    jacobi_core(sm, w, use_warm ? w.A0 : w.G);
+    jacobi_core<GA>(sm, w, use_warm ? w.A0 : w.G, w.T);
 }
 
 // ---- 4. V_new = V_old J_1 ... J_R, 64 rows per 1024-thread workgroup, rows in LDS ------------
@@ -373,13 +397,20 @@ __global__ __launch_bounds__(kJacobiThreads) void k_jacobi_lds(SvtWs w, int warm
 constexpr int kVRows = 64;
 constexpr int kLogRounds = 16;
 
-// Rows i0 .. i0+63 of Vn = Vo J_1 ... J_R (Vo = identity when null); 1024 threads.
+// Rows i0 .. i0 + vrows - 1 of Vn = Vo J_1 ... J_R (Vo = identity when null); 1024 threads.
+// vrows = kVRows, or half that where 64 rows of Bp > kLdsMaxBp exceed the LDS (vrebuild_rows).
+__host__ __device__ constexpr int vrebuild_rows(int Bp) { return Bp <= kLdsMaxBp ? kVRows : kVRows / 2; }
+__host__ __device__ constexpr size_t vrebuild_lds(int Bp) {
+    return sizeof(double) * ((size_t)vrebuild_rows(Bp) * Bp + (size_t)kLogRounds * (Bp / 2) * 2) +
+           sizeof(short) * (size_t)kLogRounds * (Bp / 2) * 2;
+}
+
 __device__ __noinline__ void vrebuild_tile(double *vsm, SvtWs w, const double *Vo, double *Vn, int i0) {
-    const int Bp = (int)w.Bp, half = Bp / 2;
-    double *vrow = vsm;                                   // [kVRows][Bp]
-    double *lcs = vrow + kVRows * Bp;                     // [kLogRounds][half][2]
+    const int Bp = (int)w.Bp, half = Bp / 2, vrows = vrebuild_rows(Bp);
+    double *vrow = vsm;                                   // [vrows][Bp]
+    double *lcs = vrow + vrows * Bp;                      // [kLogRounds][half][2]
     short *lpq = (short *)(lcs + kLogRounds * half * 2);  // [kLogRounds][half][2]
-    const int nrows = min(kVRows, Bp - i0);
+    const int nrows = min(vrows, Bp - i0);
     for (int idx = threadIdx.x; idx < nrows * Bp; idx += 1024) {
         const int rr = idx / Bp, j = idx % Bp, i = i0 + rr;
         vrow[rr * Bp + j] = Vo ? Vo[(int64_t)i * Bp + j] : (i == j ? 1.0 : 0.0);
@@ -428,7 +459,7 @@ __global__ __launch_bounds__(1024) void k_jacobi_vrebuild(SvtWs w, int warm) {
     extern __shared__ double vsm[];
     const bool use_warm = warm && w.state[0] == 1;
     const int cur = w.state[1];
-    vrebuild_tile(vsm, w, use_warm ? w.V[cur] : nullptr, w.V[cur ^ 1], blockIdx.x * kVRows);
+    vrebuild_tile(vsm, w, use_warm ? w.V[cur] : nullptr, w.V[cur ^ 1], blockIdx.x * vrebuild_rows((int)w.Bp));
 }
 
 __global__ void k_svt_finish_state(SvtWs w) {
@@ -497,11 +528,14 @@ __device__ __forceinline__ void eig_bounds(const double *A, int n, double &gl, d
 
 // D + F of the chain (one workgroup): the certificate on V = w.V[0], at most 3 Newton-Schulz
 // steps, the Jacobi fallback, then E.  res = this thread's eigenvector residual (thread i < n).
+// NB: the fp64 products' block count (eig_nb); GA: the fallback's packed triangle in w.T (free once
+// the back-transformation has consumed W) instead of LDS.
+template <int NB, bool GA>
 __device__ __forceinline__ void eig_certify_finish(double *sm, double *red, const SvtWs &w, int n, int B, double tau,
                                                    double tn, double res, int dbg, unsigned long long *ts) {
     const int tid = threadIdx.x;
     int cur = 0;
-    double dev = eig_syrk<true, 1>(sm, w.V[0], n, nullptr, 0.0, 0, nullptr, w.A0, red);
+    double dev = eig_syrk<true, 1, NB>(sm, w.V[0], n, nullptr, 0.0, 0, nullptr, w.A0, red);
     bool bad = !(dev <= kEigOrth0);
     if (!bad) {
         double mix = 0.0;
@@ -516,9 +550,9 @@ __device__ __forceinline__ void eig_certify_finish(double *sm, double *red, cons
         bad = __syncthreads_or(!(bound <= kEigRes * tn));
     }
     for (int step = 0; step < 3 && !bad && dev > kEigOrth; ++step) {
-        eig_ns_step(sm, w.V[cur], w.A0, n, w.V[cur ^ 1]);
+        eig_ns_step<NB>(sm, w.V[cur], w.A0, n, w.V[cur ^ 1]);
         cur ^= 1;
-        dev = eig_syrk<true, 1>(sm, w.V[cur], n, nullptr, 0.0, 0, nullptr, w.A0, red);
+        dev = eig_syrk<true, 1, NB>(sm, w.V[cur], n, nullptr, 0.0, 0, nullptr, w.A0, red);
     }
     bad = bad || !(dev <= kEigOrth);
     if (ts && tid == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
@@ -529,9 +563,9 @@ __device__ __forceinline__ void eig_certify_finish(double *sm, double *red, cons
     if (bad) {
         // clustered / repeated eigenvalues: the orthogonal Jacobi basis of the same G
         __syncthreads();
-        jacobi_core(sm, w, w.G);
+        jacobi_core<GA>(sm, w, w.G, w.T);
         cur = 0;
-        for (int i0 = 0; i0 < n; i0 += kVRows) {
+        for (int i0 = 0; i0 < n; i0 += vrebuild_rows(n)) {
             vrebuild_tile(sm, w, nullptr, w.V[0], i0);
             __syncthreads();
         }
@@ -542,21 +576,25 @@ __device__ __forceinline__ void eig_certify_finish(double *sm, double *red, cons
         w.state[4] = bad ? 2 : 1;
     }
     __syncthreads();
-    eig_syrk<false, 0>(sm, w.V[cur], n, w.lam, tau, B, w.E, nullptr, red, w.Fp);
+    eig_syrk<false, 0, NB>(sm, w.V[cur], n, w.lam, tau, B, w.E, nullptr, red, w.Fp);
     if (ts && tid == 0) ts[6] = __builtin_amdgcn_s_memrealtime();
 }
 
+// GA (B > kLdsMaxBp): the packed A (reflectors + T) in w.A0, dead once the back-transformation is
+// done (the certificate then writes S there), the LDS holding only the vectors and the products'
+// staging
+template <int NB, bool GA>
 __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double tau, int dbg) {
     extern __shared__ double sm[];
     __shared__ double shb[2], red[kEigThreads / 64];
     const int n = (int)w.Bp, tid = threadIdx.x;
     unsigned long long *ts = (unsigned long long *)(w.state + 16);   // phase timestamps (100 MHz)
     if (tid == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
-    double *A = sm;
-    double *pv = A + (size_t)n * (n + 1) / 2;      // [n] p vector, then the eigenvalues
+    double *A = GA ? w.A0 : sm;
+    double *pv = GA ? sm : A + (size_t)n * (n + 1) / 2;   // [n] p vector, then the eigenvalues
     eig_load_packed(w.G, A, n);
     __syncthreads();
-    eig_tridiag(A, pv, shb, n, w.beta);
+    eig_tridiag<GA>(A, pv, shb, n, w.beta);
     if (tid == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
     if (dbg)   // diagnostics: the tridiagonal T (d, e) into the Gram partial buffer
         for (int j = tid; j < n; j += kEigThreads) {
@@ -578,7 +616,7 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double 
     __syncthreads();
     if (tid == 0) ts[4] = __builtin_amdgcn_s_memrealtime();
     // certificate + orthogonalisation (LDS of the reflectors is free from here on)
-    eig_certify_finish(sm, red, w, n, B, tau, tn, res, dbg, ts);
+    eig_certify_finish<NB, GA>(sm, red, w, n, B, tau, tn, res, dbg, ts);
 }
 
 // ---- 3''. the same chain over several workgroups (LRS_SVT_MULTI_WG) ---------------------------
@@ -590,16 +628,18 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig(SvtWs w, int B, double 
 // shard): beside a chip-filling sparse-coding kernel the one-workgroup chain is the
 // better choice (each launch here waits for free CUs).  Packed A (reflectors + T) passes through
 // w.A0 (free until the certificate), the residuals through w.partial.
+template <bool GA>
 __global__ __launch_bounds__(kEigThreads) void k_svt_eig_tri(SvtWs w) {
     extern __shared__ double sm[];
     __shared__ double shb[2];
     const int n = (int)w.Bp, tid = threadIdx.x;
-    double *A = sm;
-    double *pv = A + (size_t)n * (n + 1) / 2;
+    double *A = GA ? w.A0 : sm;   // GA: reduced in place in the workspace
+    double *pv = GA ? sm : A + (size_t)n * (n + 1) / 2;
     eig_load_packed(w.G, A, n);
     __syncthreads();
-    eig_tridiag(A, pv, shb, n, w.beta);
+    eig_tridiag<GA>(A, pv, shb, n, w.beta);
     __syncthreads();
+    if (GA) return;
     const int np = n * (n + 1) / 2;
     for (int e = tid; e < np; e += kEigThreads) w.A0[e] = A[e];
 }
@@ -626,6 +666,7 @@ __global__ __launch_bounds__(256) void k_svt_eig_back(SvtWs w) {
     eig_backtransform(w.A0, w.beta, (int)w.Bp, w.T, w.V[0], 4 * blockIdx.x, 4 * gridDim.x);
 }
 
+template <int NB, bool GA>
 __global__ __launch_bounds__(kEigThreads) void k_svt_eig_cert(SvtWs w, int B, double tau) {
     extern __shared__ double sm[];
     __shared__ double red[kEigThreads / 64];
@@ -634,7 +675,7 @@ __global__ __launch_bounds__(kEigThreads) void k_svt_eig_cert(SvtWs w, int B, do
     double gl, gu, tn, pivmin;
     eig_bounds(w.A0, n, gl, gu, tn, pivmin);   // from the packed A, before the certificate reuses A0
     __syncthreads();
-    eig_certify_finish(sm, red, w, n, B, tau, tn, res, 0, nullptr);
+    eig_certify_finish<NB, GA>(sm, red, w, n, B, tau, tn, res, 0, nullptr);
 }
 
 // ---- 5a. E = V diag(e) V^T, e_k = min(tau/s_k, 1); s_out = sorted singular values -----------
@@ -691,12 +732,15 @@ __global__ __launch_bounds__(256) void k_sorted_singular_values(SvtWs w, int B, 
 // was written in that order by the eigensolver (Fp, store_fp): each B fragment is 64 consecutive
 // floats out of L2.  No LDS, so several waves per SIMD hide the memory latency; Z is read once and
 // U written once.  Exact f32 products, fp32 accumulation.
-constexpr int kApTiles = 13, kApRows = 1;   // accumulator tiles per wave: 16 kApRows rows x 13 x 16 columns
+// Accumulator tiles per wave: 16 kApRows rows x NTL x 16 columns (NTL = 13 up to B = 208, 16 up to
+// 256), NST = ap_steps(B) k-steps.
+constexpr int kApRows = 1;
 
-template <int RT>
+template <int RT, int NTL = 13, int NST = 50>
 __global__ __launch_bounds__(256) void k_svt_apply_f(const float *__restrict__ X, const float *__restrict__ L2,
                                                      float c2, const float *__restrict__ Fp, int64_t P, int B,
                                                      float *__restrict__ U) {
+    constexpr int kApTiles = NTL, kApSteps = NST;
     const int lane = threadIdx.x & 63, g = lane >> 4, jl = lane & 15;
     const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (16 * RT);
     if (r0 >= P) return;
@@ -737,7 +781,8 @@ __global__ __launch_bounds__(256) void k_svt_apply_f(const float *__restrict__ X
 #pragma unroll
             for (int t = 0; t < kApTiles; ++t) {
                 const int c = 16 * t + jl;
-                const float b = c < B ? fb[c * 4] : 0.0f;
+                // rows k >= B of F are never written (the workspace's zeros): skip them explicitly
+                const float b = (c < B && k + h < B) ? fb[c * 4] : 0.0f;
 #pragma unroll
                 for (int m = 0; m < RT; ++m) acc[m][t] = mfma16x16x4(h ? z[m].y : z[m].x, b, acc[m][t]);
             }
@@ -790,10 +835,16 @@ extern "C" int lrs_svt_gram_f32(const float *X, const float *L2, float c2, int64
     const int Bp = (int)w.Bp;
     int64_t rows = ((P + kGramSlabs - 1) / kGramSlabs + 3) / 4 * 4;
     const int nslab = (int)((P + rows - 1) / rows);
-    hipLaunchKernelGGL(k_gram_mfma, dim3((unsigned)nslab), dim3(256), 0, st, X, L2, c2, P, (int)B, rows, w.partial);
+    const int nt = gram_nt(B);
+    if (nt == 13)
+        hipLaunchKernelGGL((k_gram_mfma<13, 4>), dim3((unsigned)nslab), dim3(256), 0, st, X, L2, c2, P, (int)B, rows,
+                           w.partial);
+    else
+        hipLaunchKernelGGL((k_gram_mfma<16, 8>), dim3((unsigned)nslab), dim3(512), 0, st, X, L2, c2, P, (int)B, rows,
+                           w.partial);
     LRS_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_gram_reduce16, dim3((unsigned)((Bp * Bp + 255) / 256)), dim3(256), 0, st, w.partial, nslab,
-                       kGramNt, (int)B, Bp, w.G);
+                       nt, (int)B, Bp, w.G);
     LRS_CHECK_LAUNCH();
     if ((warm & LRS_SVT_WARM) && (warm & LRS_SVT_JACOBI)) {
         // A0 = V^T (G V) with the current V (unused when V is not valid yet: Jacobi starts from G)
@@ -815,22 +866,26 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
     hipStream_t st = (hipStream_t)stream;
     SvtWs w = svt_ws_layout(ws, P, B);
     const int Bp = (int)w.Bp;
-    const size_t smem = sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp + 16) + sizeof(int) * (2 * Bp);
-    const size_t vsmem = sizeof(double) * ((size_t)kVRows * Bp + (size_t)kLogRounds * (Bp / 2) * 2) +
-                         sizeof(short) * (size_t)kLogRounds * (Bp / 2) * 2;
+    const bool ga = Bp > kLdsMaxBp;   // the packed triangle in the workspace, not in LDS
+    const int nb = eig_nb(Bp);
+    // LDS of the Jacobi solve: the packed triangle (unless ga) + its rotation tables
+    const size_t jaux = sizeof(double) * ((size_t)Bp + 16) + sizeof(int) * (2 * Bp);
+    const size_t smem = (ga ? 0 : sizeof(double) * (size_t)Bp * (Bp + 1) / 2) + jaux;
+    const size_t vsmem = vrebuild_lds(Bp);
     if (warm & LRS_SVT_JACOBI) {
         const int jwarm = warm & LRS_SVT_WARM;
         // dynamic LDS above 64 KiB must be opted into; request exactly what this shape needs
-        hipError_t ea = hipFuncSetAttribute((const void *)k_jacobi_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)smem);
+        const void *kj = ga ? (const void *)k_jacobi_lds<true> : (const void *)k_jacobi_lds<false>;
+        hipError_t ea = hipFuncSetAttribute(kj, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (ea != hipSuccess) return (int)ea;
         ea = hipFuncSetAttribute((const void *)k_jacobi_vrebuild, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)vsmem);
         if (ea != hipSuccess) return (int)ea;
-        hipLaunchKernelGGL(k_jacobi_lds, dim3(1), dim3(kJacobiThreads), smem, st, w, jwarm);
+        if (ga) hipLaunchKernelGGL(k_jacobi_lds<true>, dim3(1), dim3(kJacobiThreads), smem, st, w, jwarm);
+        else hipLaunchKernelGGL(k_jacobi_lds<false>, dim3(1), dim3(kJacobiThreads), smem, st, w, jwarm);
         LRS_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_jacobi_vrebuild, dim3((unsigned)((Bp + kVRows - 1) / kVRows)), dim3(1024), vsmem, st,
-                           w, jwarm);
+        const int vr = vrebuild_rows(Bp);
+        hipLaunchKernelGGL(k_jacobi_vrebuild, dim3((unsigned)((Bp + vr - 1) / vr)), dim3(1024), vsmem, st, w, jwarm);
         LRS_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_svt_finish_state, dim3(1), dim3(1), 0, st, w);
         LRS_CHECK_LAUNCH();
@@ -838,17 +893,21 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
                            w, (int)B, tau);
         LRS_CHECK_LAUNCH();
     } else {
-        const size_t tsmem = sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp);
-        const size_t esmem = sizeof(double) * 2 * kEKc * kELd;
+        const size_t tsmem = sizeof(double) * ((ga ? 0 : (size_t)Bp * (Bp + 1) / 2) + Bp);
+        const size_t esmem = sizeof(double) * 2 * kEKc * eld(nb);
         const size_t lds = std::max(std::max(tsmem, esmem), std::max(smem, vsmem));
+        // the instantiations: (NB, GA) = (7, false) up to kLdsMaxBp, (7, true) up to 224, (8, true) above
+        const void *keig = nb == 8 ? (const void *)k_svt_eig<8, true>
+                                   : ga ? (const void *)k_svt_eig<7, true> : (const void *)k_svt_eig<7, false>;
+        const void *kcert = nb == 8 ? (const void *)k_svt_eig_cert<8, true>
+                                    : ga ? (const void *)k_svt_eig_cert<7, true> : (const void *)k_svt_eig_cert<7, false>;
         if (warm & LRS_SVT_MULTI_WG) {
-            hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig_tri, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                (int)tsmem);
-            if (ea == hipSuccess)
-                ea = hipFuncSetAttribute((const void *)k_svt_eig_cert, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)lds);
+            const void *ktri = ga ? (const void *)k_svt_eig_tri<true> : (const void *)k_svt_eig_tri<false>;
+            hipError_t ea = hipFuncSetAttribute(ktri, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tsmem);
+            if (ea == hipSuccess) ea = hipFuncSetAttribute(kcert, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (ea != hipSuccess) return (int)ea;
-            hipLaunchKernelGGL(k_svt_eig_tri, dim3(1), dim3(kEigThreads), tsmem, st, w);
+            if (ga) hipLaunchKernelGGL(k_svt_eig_tri<true>, dim3(1), dim3(kEigThreads), tsmem, st, w);
+            else hipLaunchKernelGGL(k_svt_eig_tri<false>, dim3(1), dim3(kEigThreads), tsmem, st, w);
             LRS_CHECK_LAUNCH();
             hipLaunchKernelGGL(k_svt_eig_vals, dim3((unsigned)((4 * Bp + kEigMwThreads - 1) / kEigMwThreads)),
                                dim3(kEigMwThreads), 0, st, w);
@@ -858,13 +917,16 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
             LRS_CHECK_LAUNCH();
             hipLaunchKernelGGL(k_svt_eig_back, dim3((unsigned)((Bp + 15) / 16)), dim3(256), 0, st, w);
             LRS_CHECK_LAUNCH();
-            hipLaunchKernelGGL(k_svt_eig_cert, dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau);
+            if (nb == 8) hipLaunchKernelGGL((k_svt_eig_cert<8, true>), dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau);
+            else if (ga) hipLaunchKernelGGL((k_svt_eig_cert<7, true>), dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau);
+            else hipLaunchKernelGGL((k_svt_eig_cert<7, false>), dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau);
             LRS_CHECK_LAUNCH();
         } else {
-            hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                (int)lds);
+            hipError_t ea = hipFuncSetAttribute(keig, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (ea != hipSuccess) return (int)ea;
-            hipLaunchKernelGGL(k_svt_eig, dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau, 0);
+            if (nb == 8) hipLaunchKernelGGL((k_svt_eig<8, true>), dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau, 0);
+            else if (ga) hipLaunchKernelGGL((k_svt_eig<7, true>), dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau, 0);
+            else hipLaunchKernelGGL((k_svt_eig<7, false>), dim3(1), dim3(kEigThreads), lds, st, w, (int)B, tau, 0);
             LRS_CHECK_LAUNCH();
         }
     }
@@ -872,8 +934,11 @@ extern "C" int lrs_svt_finish_f32(const float *X, const float *L2, float c2, int
         hipLaunchKernelGGL(k_sorted_singular_values, dim3(1), dim3(256), 0, st, w, (int)B, s_out);
         LRS_CHECK_LAUNCH();
     }
-    hipLaunchKernelGGL(k_svt_apply_f<kApRows>, dim3((unsigned)((P + 64 * kApRows - 1) / (64 * kApRows))), dim3(256), 0,
-                       st, X, L2, c2, w.Fp, P, (int)B, U);
+    const dim3 agrid((unsigned)((P + 64 * kApRows - 1) / (64 * kApRows)));
+    if (B <= 200)
+        hipLaunchKernelGGL((k_svt_apply_f<kApRows, 13, 50>), agrid, dim3(256), 0, st, X, L2, c2, w.Fp, P, (int)B, U);
+    else
+        hipLaunchKernelGGL((k_svt_apply_f<kApRows, 16, 64>), agrid, dim3(256), 0, st, X, L2, c2, w.Fp, P, (int)B, U);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -899,12 +964,14 @@ extern "C" int lrs_diag_svt_state(void *ws, int64_t P, int64_t B, int *out32) {
 extern "C" int lrs_diag_svt_eig(void *ws, int64_t P, int64_t B, double *out, void *stream) {
     SvtWs w = svt_ws_layout(ws, P, B);
     const int Bp = (int)w.Bp;
+    if (Bp > kLdsMaxBp) return LRS_E_UNSUPPORTED;   // diagnostics of the LDS-resident chain only
     const size_t smem = std::max(sizeof(double) * ((size_t)Bp * (Bp + 1) / 2 + Bp + 16) + sizeof(int) * (2 * Bp),
                                  sizeof(double) * 2 * kEKc * kELd);
-    hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipError_t ea = hipFuncSetAttribute((const void *)k_svt_eig<7, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)smem);
     if (ea != hipSuccess) return (int)ea;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_svt_eig, dim3(1), dim3(kEigThreads), smem, st, w, (int)B, 1.0, 1);
+    hipLaunchKernelGGL((k_svt_eig<7, false>), dim3(1), dim3(kEigThreads), smem, st, w, (int)B, 1.0, 1);
     LRS_CHECK_LAUNCH();
     // out: d[Bp], e[Bp], lam[Bp], W[Bp*Bp], V[Bp*Bp], S[Bp*Bp]
     hipError_t e = hipStreamSynchronize(st);
@@ -926,6 +993,7 @@ extern "C" int lrs_diag_svt_apply(const float *X, const float *L2, float c2, int
                                   int dbg, void *stream) {
     SvtWs w = svt_ws_layout(ws, P, B);
     hipStream_t st = (hipStream_t)stream;
+    if (B > 200) return LRS_E_UNSUPPORTED;   // diagnostics of the B <= 200 apply variants only
     if (dbg == 1)
         hipLaunchKernelGGL(k_svt_apply_f<1>, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, st, X, L2, c2, w.Fp, P,
                            (int)B, U);

@@ -66,10 +66,20 @@ __device__ __forceinline__ double wdist(const double (&r)[4], int j) {
     return t == 0 ? v0 : t == 1 ? v1 : t == 2 ? v2 : v3;
 }
 
-// ---- A. tridiagonalisation: A (packed, LDS) -> T on its diagonal / first superdiagonal --------
+// Workgroup barrier of the chain: LDS-only while the packed A is in LDS (B <= kLdsMaxBp), a full
+// one (global stores drained and visible to the workgroup) when A lives in the workspace.
+template <bool GA>
+__device__ __forceinline__ void eig_bar() {
+    if (GA) __syncthreads();
+    else lds_barrier();
+}
+
+// ---- A. tridiagonalisation: A (packed) -> T on its diagonal / first superdiagonal ---------------
 // Per column k: wave 0 forms the reflector; the matvec p = beta A_sub v runs four threads per row
 // with eight loads in flight per thread; the rank-2 update runs one wave per row over absolute
-// column lanes (v_j, w_j computed once per lane), two rows per batch.
+// column lanes (v_j, w_j computed once per lane), two rows per batch.  GA: A is in global memory
+// (the workspace, L2-resident: B > kLdsMaxBp, whose packed triangle exceeds the 160 KiB of LDS).
+template <bool GA>
 __device__ __noinline__ void eig_tridiag(double *A, double *pv, double *shb, int n, double *beta_g) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int NW = kEigThreads / 64;
@@ -105,7 +115,7 @@ __device__ __noinline__ void eig_tridiag(double *A, double *pv, double *shb, int
                 beta_g[k] = beta;
             }
         }
-        lds_barrier();
+        eig_bar<GA>();
         const double beta = shb[k & 1];
         if (beta == 0.0) continue;   // column already reduced (uniform branch)
         // p = beta * A_sub v, four threads per row, quad reduction
@@ -136,7 +146,7 @@ __device__ __noinline__ void eig_tridiag(double *A, double *pv, double *shb, int
             acc += __shfl_xor(acc, 2, 64);
             if (i < n && q == 0) pv[i] = beta * acc;
         }
-        lds_barrier();
+        eig_bar<GA>();
         // K = beta/2 p.v (every wave computes the same value), w = p - K v
         double vj[4], wj[4], kp = 0.0;
 #pragma unroll
@@ -179,7 +189,7 @@ __device__ __noinline__ void eig_tridiag(double *A, double *pv, double *shb, int
                 }
             }
         }
-        lds_barrier();
+        eig_bar<GA>();
     }
 }
 
@@ -439,13 +449,18 @@ __device__ __forceinline__ void store_fp(float *Fp, int B, int k, int c, float e
 
 // ---- one-workgroup fp64 products on a 32 x 32 thread grid -------------------------------------
 // Operands staged kEKc values of the summation index at a time as [kk][row] images (row stride
-// kELd = 225 doubles: the transposed staging stores hit distinct banks).  Thread (ty, tx) owns
-// rows ty + 32a and columns tx + 32b of the n x n result (n <= 224).
-constexpr int kEKc = 16, kELd = 225;
+// eld(NB) = 32 NB + 1 doubles: the transposed staging stores hit distinct banks).  Thread (ty, tx)
+// owns rows ty + 32a and columns tx + 32b of the n x n result (n <= 32 NB: NB = 7 up to 224, 8 up
+// to 256; the sums run over k in the same order either way).
+constexpr int kEKc = 16;
+__host__ __device__ constexpr int eld(int NB) { return 32 * NB + 1; }
+constexpr int kELd = eld(7);
+__host__ __device__ constexpr int eig_nb(int n) { return n <= 224 ? 7 : 8; }
 
-// stage X(k0 + kk, r) for kk < kEKc, r < kELd (zero outside n): KMAJ: X[k * ld + r], else X[r * ld + k]
-template <bool KMAJ>
+// stage X(k0 + kk, r) for kk < kEKc, r < LD (zero outside n): KMAJ: X[k * ld + r], else X[r * ld + k]
+template <bool KMAJ, int NB = 7>
 __device__ __forceinline__ void eig_stage(double *Xs, const double *X, int ld, int n, int k0) {
+    constexpr int kELd = eld(NB);
     constexpr int NIT = (kEKc * kELd + kEigThreads - 1) / kEigThreads;
     double v[NIT];
 #pragma unroll
@@ -471,20 +486,21 @@ __device__ __forceinline__ void eig_stage(double *Xs, const double *X, int ld, i
 // Symmetric product C = X^T diag(f) X over the summation index k (X(k, r) as eig_stage<KMAJ>),
 // blocks a <= b only.  MODE 0: f_k = min(tau / sqrt(lam_k), 1), C -> E (float, B x B);
 // MODE 1: f = 1, C -> S (double, n x n) and the return value is max |S - I| (uniform).
-template <bool KMAJ, int MODE>
+template <bool KMAJ, int MODE, int NB = 7>
 __device__ __noinline__ double eig_syrk(double *sm, const double *X, int n, const double *lam, double tau, int B,
                                         float *E, double *S, double *red, float *Fp = nullptr) {
+    constexpr int kELd = eld(NB);
     double *Xs = sm;                   // [kEKc][kELd]
     double *Xf = sm + kEKc * kELd;     // [kEKc][kELd]  X * f  (MODE 0)
     const int tid = threadIdx.x, ty = tid >> 5, tx = tid & 31;
-    double acc[7][7];
+    double acc[NB][NB];
 #pragma unroll
-    for (int a = 0; a < 7; ++a)
+    for (int a = 0; a < NB; ++a)
 #pragma unroll
-        for (int b = 0; b < 7; ++b) acc[a][b] = 0.0;
+        for (int b = 0; b < NB; ++b) acc[a][b] = 0.0;
     for (int k0 = 0; k0 < n; k0 += kEKc) {
         __syncthreads();
-        eig_stage<KMAJ>(Xs, X, n, n, k0);
+        eig_stage<KMAJ, NB>(Xs, X, n, n, k0);
         if (MODE == 0) {
             __syncthreads();
             for (int idx = tid; idx < kEKc * kELd; idx += kEigThreads) {
@@ -503,14 +519,14 @@ __device__ __noinline__ double eig_syrk(double *sm, const double *X, int n, cons
         const int kn = min(kEKc, n - k0);
 #pragma unroll 2
         for (int kk = 0; kk < kn; ++kk) {
-            double vj[7];
+            double vj[NB];
 #pragma unroll
-            for (int b = 0; b < 7; ++b) vj[b] = Xs[kk * kELd + tx + 32 * b];
+            for (int b = 0; b < NB; ++b) vj[b] = Xs[kk * kELd + tx + 32 * b];
 #pragma unroll
-            for (int a = 0; a < 7; ++a) {
+            for (int a = 0; a < NB; ++a) {
                 const double vi = Xl[kk * kELd + ty + 32 * a];
 #pragma unroll
-                for (int b = a; b < 7; ++b) acc[a][b] = __fma_rn(vi, vj[b], acc[a][b]);
+                for (int b = a; b < NB; ++b) acc[a][b] = __fma_rn(vi, vj[b], acc[a][b]);
             }
         }
     }
@@ -518,9 +534,9 @@ __device__ __noinline__ double eig_syrk(double *sm, const double *X, int n, cons
     // by the thread with tx >= ty, so C is bitwise symmetric.
     double dmax = 0.0;
 #pragma unroll
-    for (int a = 0; a < 7; ++a)
+    for (int a = 0; a < NB; ++a)
 #pragma unroll
-        for (int b = a; b < 7; ++b) {
+        for (int b = a; b < NB; ++b) {
             const int i = ty + 32 * a, j = tx + 32 * b;
             const int lim = MODE == 0 ? B : n;
             if (i < lim && j < lim && (a != b || tx >= ty)) {
@@ -550,41 +566,43 @@ __device__ __noinline__ double eig_syrk(double *sm, const double *X, int n, cons
 }
 
 // One Newton-Schulz (Loewdin) orthogonalisation step Vn = 1.5 V - 0.5 V S with S = V^T V
-// (V[r * n + c], S symmetric).  Two passes over the row blocks keep the accumulators at 28.
+// (V[r * n + c], S symmetric).  Two passes over the row blocks keep the accumulators at 4 NB.
+template <int NB = 7>
 __device__ __noinline__ void eig_ns_step(double *sm, const double *V, const double *S, int n, double *Vn) {
+    constexpr int kELd = eld(NB);
     double *As = sm;                   // [kEKc][kELd]  V(r, j) for the chunk of j
     double *Bs = sm + kEKc * kELd;     // [kEKc][kELd]  S(j, c)
     const int tid = threadIdx.x, ty = tid >> 5, tx = tid & 31;
     for (int half = 0; half < 2; ++half) {
-        const int a0 = half * 4, na = half == 0 ? 4 : 3;
-        double acc[4][7];
+        const int a0 = half * 4, na = half == 0 ? 4 : NB - 4;
+        double acc[4][NB];
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 7; ++b) acc[a][b] = 0.0;
+            for (int b = 0; b < NB; ++b) acc[a][b] = 0.0;
         for (int k0 = 0; k0 < n; k0 += kEKc) {
             __syncthreads();
-            eig_stage<false>(As, V, n, n, k0);
-            eig_stage<true>(Bs, S, n, n, k0);
+            eig_stage<false, NB>(As, V, n, n, k0);
+            eig_stage<true, NB>(Bs, S, n, n, k0);
             __syncthreads();
             const int kn = min(kEKc, n - k0);
 #pragma unroll 2
             for (int kk = 0; kk < kn; ++kk) {
-                double vj[7];
+                double vj[NB];
 #pragma unroll
-                for (int b = 0; b < 7; ++b) vj[b] = Bs[kk * kELd + tx + 32 * b];
+                for (int b = 0; b < NB; ++b) vj[b] = Bs[kk * kELd + tx + 32 * b];
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
                     const double vi = (a < na) ? As[kk * kELd + ty + 32 * (a0 + a)] : 0.0;
 #pragma unroll
-                    for (int b = 0; b < 7; ++b) acc[a][b] = __fma_rn(vi, vj[b], acc[a][b]);
+                    for (int b = 0; b < NB; ++b) acc[a][b] = __fma_rn(vi, vj[b], acc[a][b]);
                 }
             }
         }
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 7; ++b) {
+            for (int b = 0; b < NB; ++b) {
                 const int r = ty + 32 * (a0 + a), c = tx + 32 * b;
                 if (a < na && r < n && c < n) {
                     const int64_t o = (int64_t)r * n + c;

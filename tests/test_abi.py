@@ -70,7 +70,11 @@ def test_invalid_arguments_rejected():
     L = _lib.lib()
     off, ld = ctypes.c_int64(), ctypes.c_int64()
     assert L.lrs_svt_gram_offset(4000, 198, ctypes.byref(off), ctypes.byref(ld)) == 0 and ld.value == 198
-    assert L.lrs_svt_gram_offset(4000, 199, ctypes.byref(off), ctypes.byref(ld)) == -2   # B <= 198
+    # B <= 256: up to 198 bands the eigensolver's packed triangle is in LDS, above it in the workspace
+    assert L.lrs_svt_gram_offset(4000, 199, ctypes.byref(off), ctypes.byref(ld)) == 0 and ld.value == 200
+    assert L.lrs_svt_gram_offset(4000, 224, ctypes.byref(off), ctypes.byref(ld)) == 0 and ld.value == 224
+    assert L.lrs_svt_gram_offset(4000, 256, ctypes.byref(off), ctypes.byref(ld)) == 0
+    assert L.lrs_svt_gram_offset(4000, 257, ctypes.byref(off), ctypes.byref(ld)) == -2
     assert L.lrs_block_count(10, 10, 20, 20) < 0
     assert L.lrs_ista_f32(None, None, None, 64, 64, 256, 10, None, None, 10, 0, None, None, None, None, 0,
                           None) == -1

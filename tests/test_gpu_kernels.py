@@ -387,7 +387,11 @@ def test_alpha_kernel_vs_numpy(ops, n, variant):
 # ------------------------------------------------------------------------------------------ SVT
 @pytest.mark.parametrize("method", ["tri", "jacobi"])
 @pytest.mark.parametrize("P,B,rank,noise", [(1296, 128, 8, 0.12), (4000, 198, 8, 0.02), (500, 60, 3, 0.002),
-                                            (777, 45, 5, 0.05)])
+                                            (777, 45, 5, 0.05),
+                                            # above 198 bands the packed triangle lives in the workspace
+                                            # (the 224-band cubes of configs[3]/[4]); 256 is the limit
+                                            (3000, 199, 8, 0.02), (3000, 200, 8, 0.02), (5000, 224, 8, 0.02),
+                                            (4096, 256, 8, 0.02)])
 def test_svt_kernel_vs_numpy(ops, P, B, rank, noise, method):
     rng = np.random.default_rng(P + B)
     Z = (rng.random((P, rank)) @ rng.random((rank, B)) * 0.3 + noise * rng.standard_normal((P, B)))
@@ -411,7 +415,7 @@ def test_svt_kernel_vs_numpy(ops, P, B, rank, noise, method):
     assert rel(U2, O.svt(X2 + c2 * L2, 1 / 0.9)) < 1e-5
 
 
-@pytest.mark.parametrize("B", [64, 197])
+@pytest.mark.parametrize("B", [64, 197, 224])
 @pytest.mark.parametrize("exact", [True, False])
 def test_svt_repeated_singular_values(ops, B, exact):
     """Repeated singular values.  exact: Z = 2 [I; 0] plus a rank-3 term on rows the identity does
@@ -441,7 +445,8 @@ def test_svt_repeated_singular_values(ops, B, exact):
     assert ops.svt_state(ws, P, B)[4] == path and np.array_equal(Um.view(np.uint32), U.view(np.uint32))
 
 
-@pytest.mark.parametrize("P,B", [(1296, 128), (4000, 198), (500, 60), (777, 45), (300, 7), (2000, 197)])
+@pytest.mark.parametrize("P,B", [(1296, 128), (4000, 198), (500, 60), (777, 45), (300, 7), (2000, 197),
+                                 (3000, 224), (3000, 255)])
 def test_svt_multi_workgroup_bit_identical(ops, P, B):
     """LRS_SVT_MULTI_WG (the eigenvalue, inverse-iteration and back-transformation phases over many
     workgroups, for a row-slab shard whose eigensolver is on the critical path): U and the singular
