@@ -634,6 +634,26 @@ __device__ __forceinline__ void block_sum3_d(double &a, double &b, double &c, do
 // ------------------------------------------------------------------------------------------
 constexpr int kBnThreads = 256;
 constexpr int kBn1Threads = 1024;   // one workgroup per channel (S == 1): 16 waves share the channel
+// ... and on small maps (P <= 4 * kBn1Small: the 25^2 and smaller maps at 196^2, 18^2 and smaller at
+// 36^2), where 1024 threads would leave most lanes idle, 256 threads (bn1_threads, dipnet.hip)
+constexpr int kBn1Small = 256;
+
+// element i of a [C][P] tensor summed over nsplit split-K partials (stride MN): acc[e] = the splits
+// e, e + 8, ... in increasing order (k_gemm_reduce's order), the loads of one group of 8 predicated.
+// (Every load of up to 32 splits issued before the first add measured slower: 36^2 step 0.635 ->
+// 0.671 ms, 196^2 1.244 -> 1.272, tuning build, 2 interleaved rounds.)
+__device__ __forceinline__ float splitk_sum1(const float *__restrict__ part, int nsplit, int64_t MN, int64_t i) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int z0 = 0; z0 < nsplit; z0 += 8) {
+        float p[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) p[e] = z0 + e < nsplit ? part[(int64_t)(z0 + e) * MN + i] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (z0 + e < nsplit) acc[e] += p[e];
+    }
+    return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
 
 // c = max(max|gamma_orig|, 1.0) (lipschitz_constraint_layer.py:93-97); whole block, C <= 4 * blockDim
 __device__ float bn_lip_scale(const float *gamma, int C, float *redf) {
@@ -828,19 +848,16 @@ __global__ __launch_bounds__(kBn1Threads) void k_bn_fwd1(BnArgs a) {
 // P <= 4 * kBn1Threads): z = sum of the GEMM's split-K partials (k_gemm_reduce's order) + bias,
 // stored for the backward, then k_bn_fwd1's statistics / normalisation / activation from the
 // values held in registers.  Replaces k_gemm_reduce + k_bn_fwd1 for the small-map convs.
-__global__ __launch_bounds__(kBn1Threads) void k_reduce_bn1(const float *__restrict__ part, int nsplit,
-                                                            const float *__restrict__ bias, BnArgs a) {
-    __shared__ double red[2 * kBn1Threads / 64];
+template <int TH = kBn1Threads>
+__global__ __launch_bounds__(TH) void k_reduce_bn1(const float *__restrict__ part, int nsplit,
+                                                   const float *__restrict__ bias, BnArgs a,
+                                                   const float *__restrict__ sdiv = nullptr) {
+    __shared__ double red[2 * TH / 64];
     const int c = blockIdx.y, t = threadIdx.x;
     const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
-    auto zsum = [&](int i) {
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        int zz = 0;
-        for (; zz + 8 <= nsplit; zz += 8)
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc[q] += part[(int64_t)(zz + q) * MN + off + i];
-        for (; zz < nsplit; ++zz) acc[zz & 7] += part[(int64_t)zz * MN + off + i];
-        float v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    auto zsum = [&](int i) {   // sdiv: as k_bn_fwd_r (raw-weight conv)
+        float v = splitk_sum1(part, nsplit, MN, off + i);
+        if (sdiv) v = v / *sdiv;
         if (bias) v = v + bias[c];
         return v;
     };
@@ -848,7 +865,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn1(const float *__restr
     float zv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int i = t + u * kBn1Threads;
+        const int i = t + u * TH;
         zv[u] = 0.0f;
         if (i >= a.P) continue;
         zv[u] = zsum(i);
@@ -860,7 +877,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn1(const float *__restr
     double s1 = 0.0, s2 = 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-        if (t + u * kBn1Threads < a.P) {
+        if (t + u * TH < a.P) {
             const double d = (double)zv[u] - K;
             s1 += d;
             s2 += d * d;
@@ -871,7 +888,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn1(const float *__restr
     const float gm = a.gamma[c] / cs, bt = a.beta[c] / cs;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int i = t + u * kBn1Threads;
+        const int i = t + u * TH;
         if (i < a.P) a.y[off + i] = act_fwd((zv[u] - m32) * is32 * gm + bt, a.act);
     }
 }
@@ -1120,9 +1137,13 @@ __device__ __forceinline__ float4 splitk_sum4(const float *__restrict__ part, in
 // BN statistics, normalisation, affine (Lipschitz rescale), activation.  part == nullptr: z given.
 // TH = threads per workgroup (quads t + TH u): 1024 by default; 256 (4 wave slots instead of 16) lets a
 // 98^2 map's workgroup fit where one sparse-coding workgroup retires (tuning build, LRS_DIP_BNR_SMALL_WG)
+// sdiv (nullable): the conv ran on the raw weights W_bar (the spectral-norm scale not yet known when
+// it was launched, dipnet_step's overlapped sigma): z = sum / scale + bias, the same order as the
+// scaled path's epilogue (W / scale) x + bias up to the rounding of the quotient's place.
 template <int NQ, int TH = kBn1Threads>
 __global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part, int nsplit,
-                                                          const float *__restrict__ bias, BnArgs a) {
+                                                 const float *__restrict__ bias, BnArgs a,
+                                                 const float *__restrict__ sdiv = nullptr) {
     __shared__ double red[2 * kBn1Threads / 64];
     const int c = blockIdx.y, t = threadIdx.x;
     const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
@@ -1141,6 +1162,10 @@ __global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part,
         // acc[e] = the splits e, e + 8, ... in increasing order (k_gemm_reduce's order); the loads of
         // one group of 8 are predicated, not indexed, so acc stays in registers
         float4 v = splitk_sum4(part, nsplit, MN, off, q);
+        if (sdiv) {
+            const float sc = *sdiv;
+            v.x = v.x / sc; v.y = v.y / sc; v.z = v.z / sc; v.w = v.w / sc;
+        }
         if (bias) {
             const float b = bias[c];
             v.x = v.x + b; v.y = v.y + b; v.z = v.z + b; v.w = v.w + b;
@@ -1152,6 +1177,7 @@ __global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part,
     float k0;
     if (part) {
         k0 = splitk_sum4(part, nsplit, MN, off, 0).x;
+        if (sdiv) k0 = k0 / *sdiv;
         if (bias) k0 = k0 + bias[c];
     } else {
         k0 = z4[0].x;
@@ -1187,9 +1213,9 @@ __global__ __launch_bounds__(TH) void k_bn_fwd_r(const float *__restrict__ part,
 // thread, any P): dL/dy = the sum of the data-gradient GEMM's split-K partials (k_gemm_reduce's
 // order; dL/dy itself is not stored: only this kernel reads it), then k_bn_bwd_r's arithmetic.
 // Replaces k_gemm_reduce + k_bn_bwd1 below a small-map conv's data gradient.
-__global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__restrict__ part, int nsplit,
-                                                                BnBwdArgs a) {
-    __shared__ double red[3 * kBn1Threads / 64];
+template <int TH = kBn1Threads>
+__global__ __launch_bounds__(TH) void k_reduce_bn_bwd1(const float *__restrict__ part, int nsplit, BnBwdArgs a) {
+    __shared__ double red[3 * TH / 64];
     const int c = blockIdx.y, t = threadIdx.x;
     const int64_t MN = (int64_t)a.C * a.P, off = (int64_t)c * a.P;
     const float m32 = a.mean[c], is32 = a.invstd[c];
@@ -1200,19 +1226,10 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__r
     double sg = 0.0, sgx = 0.0, sx = 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int i = t + u * kBn1Threads;
+        const int i = t + u * TH;
         g[u] = xh[u] = 0.0f;
         if (i >= a.P) continue;
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int z0 = 0; z0 < nsplit; z0 += 8) {
-            float p[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) p[e] = z0 + e < nsplit ? part[(int64_t)(z0 + e) * MN + off + i] : 0.0f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                if (z0 + e < nsplit) acc[e] += p[e];
-        }
-        const float gy = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+        const float gy = splitk_sum1(part, nsplit, MN, off + i);
         xh[u] = (a.z[off + i] - m32) * is32;
         g[u] = bn_act_bwd(gy, xh[u], gm, bt, ldy ? a.y[off + i] : 0.0f, a);
         sg += (double)g[u];
@@ -1229,7 +1246,7 @@ __global__ __launch_bounds__(kBn1Threads) void k_reduce_bn_bwd1(const float *__r
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int i = t + u * kBn1Threads;
+        const int i = t + u * TH;
         if (i >= a.P) continue;
         const float v = k * (g[u] - mg - xh[u] * mgx);
         a.gz[off + i] = a.accum ? a.gz[off + i] + v : v;

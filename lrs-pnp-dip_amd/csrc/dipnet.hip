@@ -718,6 +718,16 @@ inline int bn_reg_q(int64_t P, bool vec) {
     return 0;
 }
 
+// Threads of a one-workgroup-per-channel BatchNorm kernel (k_reduce_bn1, k_reduce_bn_bwd1, k_bn_fwd1,
+// k_bn_bwd1): kBn1Small where the channel fits 2 values per thread of it (the 18^2 and smaller maps at
+// 36^2, the 13^2 ones at 196^2), else kBn1Threads.  A/B (tuning build, 2 rounds): 36^2 step 0.671 ->
+// 0.657 ms with 256 threads up to 1024 pixels, but the 196^2 step 1.274 -> 1.280 (its 25^2 maps then
+// hold 3 values per thread).  LRS_DIP_BN1_SMALL = the pixel limit (0: 1024 threads everywhere).
+inline int bn1_threads(int64_t P) {
+    static const int64_t lim = tune_knob("LRS_DIP_BN1_SMALL", 2 * kBn1Small);
+    return P <= lim ? kBn1Small : kBn1Threads;
+}
+
 // 98^2 maps' register BN forward on 256-thread workgroups (tuning build only; default off)
 inline bool bnr_small_wg() {
     static const bool v = tune_knob("LRS_DIP_BNR_SMALL_WG", 0) != 0;
@@ -746,7 +756,7 @@ int bn_fwd(const float *z, float *y, const float *gamma, const float *beta, floa
         LRS_BNR_SWITCH(nq, k_bn_fwd_r, dim3(1, C), dim3(kBn1Threads), 0, st, (const float *)nullptr, 0,
                        (const float *)nullptr, a);
     } else if (gamma && S == 1) {
-        hipLaunchKernelGGL(k_bn_fwd1, dim3(1, C), dim3(kBn1Threads), 0, st, a);
+        hipLaunchKernelGGL(k_bn_fwd1, dim3(1, C), dim3(bn1_threads(P)), 0, st, a);
     } else {
         if (gamma) hipLaunchKernelGGL(k_bn_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
         hipLaunchKernelGGL(k_bn_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
@@ -767,13 +777,39 @@ int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, 
     if (const int nq = gamma ? bn_reg_q(P, vec) : 0) {
         LRS_BNR_SWITCH(nq, k_bn_bwd_r, dim3(1, C), dim3(kBn1Threads), 0, st, a);
     } else if ((gamma || gbias) && S == 1) {
-        hipLaunchKernelGGL(k_bn_bwd1, dim3(1, C), dim3(kBn1Threads), 0, st, a);
+        hipLaunchKernelGGL(k_bn_bwd1, dim3(1, C), dim3(bn1_threads(P)), 0, st, a);
     } else {
         if (gamma || gbias) hipLaunchKernelGGL(k_bn_bwd_stats, dim3(S, C), dim3(kBnThreads), 0, st, a);
         hipLaunchKernelGGL(k_bn_bwd_apply, dim3(S, C), dim3(kBnThreads), 0, st, a);
     }
     LRS_CHECK_LAUNCH();
     return LRS_OK;
+}
+
+// The step head of the overlapped sigma (lrs_dipnet::sn_overlap): the spectral-norm Gram partials of
+// the n convs (blockIdx.y < n, k_sn_gram's body) and, in the extra row blockIdx.y == n, the first
+// conv's forward planes from the raw weights (the head ConvPrep) with the step's loss reset and Adam
+// step count: one launch instead of two.
+__global__ __launch_bounds__(256) void k_sn_gram_head(const SnConv *convs, double *gram, int n, const ConvPrep *head,
+                                                     double *loss_acc, int *step) {
+    __shared__ float Ws[128][36];
+    if ((int)blockIdx.y == n) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {   // a training step begins
+            *loss_acc = 0.0;
+            *step += 1;
+        }
+        conv_prep_body(*head, 1.0f, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+        return;
+    }
+    const SnConv cv = convs[blockIdx.y];
+    double *out = gram + (int64_t)blockIdx.y * kSnGramDoubles + (int64_t)kSnMaxDim * kSnMaxDim +
+                  (int64_t)blockIdx.x * kSnPairs * 256;
+    switch (threadIdx.x >> 6) {
+    case 0: sn_gram_body<0>(cv, Ws, out); break;
+    case 1: sn_gram_body<1>(cv, Ws, out); break;
+    case 2: sn_gram_body<2>(cv, Ws, out); break;
+    default: sn_gram_body<3>(cv, Ws, out); break;
+    }
 }
 
 int sn_launch(const SnConv *table_dev, int n, int64_t max_elems, double *gram, float *sigma, float *scale,
@@ -1127,6 +1163,13 @@ struct lrs_dipnet {
     int64_t dz_off = 0, dcol_off = 0, part_off = 0, part_cap = 0, sigma_off = 0, scale_off = 0;
     int64_t gram_off_bytes = 0, table_off_bytes = 0, misc_off_bytes = 0, bnpart_off_bytes = 0, prep_off_bytes = 0;
     int n_prep = 0;           // convs in the per-step weight-preparation table (spectral norm and/or planes)
+    // sigma overlapped with the first conv (dipnet_step): the side stream runs the spectral-norm
+    // chain and the preparation of every conv but the first, whose planes the main stream writes from
+    // the raw weights (prep_head table); its BatchNorm kernel divides by the scale (sn_overlap)
+    bool sn_overlap = false;
+    int n_prep_side = 0;
+    int64_t prep_head_off_bytes = 0, prep_side_off_bytes = 0;
+    hipEvent_t ev_head = nullptr, ev_sigma = nullptr;
     int64_t headcnt_off_bytes = 0;   // per-channel counters of k_mse_head (zeroed at bind, reset by the kernel)
     bool head_fusable = false;       // last node = conv without BN: loss + its activation backward in one kernel
     size_t ws_bytes = 0;
@@ -1159,6 +1202,8 @@ struct lrs_dipnet {
     double *gram() const { return (double *)(ws + gram_off_bytes); }
     SnConv *table() const { return (SnConv *)(ws + table_off_bytes); }
     ConvPrep *prep() const { return (ConvPrep *)(ws + prep_off_bytes); }
+    ConvPrep *prep_head() const { return (ConvPrep *)(ws + prep_head_off_bytes); }
+    ConvPrep *prep_side() const { return (ConvPrep *)(ws + prep_side_off_bytes); }
     int *headcnt() const { return (int *)(ws + headcnt_off_bytes); }
     double *loss_acc() const { return (double *)(ws + misc_off_bytes); }
     int *step() const { return (int *)(ws + misc_off_bytes + 8); }
@@ -1186,14 +1231,18 @@ inline int prep_blocks() {
     return v;
 }
 
-int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_begin = false) {
+// raw_first (dipnet_step's overlapped sigma, lrs_dipnet::sn_overlap): the spectral-norm chain and
+// the weight preparation were enqueued by the caller (the first conv's planes from the raw weights on
+// st, the rest on the side stream, which records ev_sigma); the first conv runs on the raw planes and
+// st waits for ev_sigma before its BatchNorm kernel, which divides by the scale.
+int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_begin = false, bool raw_first = false) {
     int rc;
-    if (net->n_sn) {
+    if (net->n_sn && !raw_first) {
         rc = sn_launch(net->table(), net->n_sn, net->max_w, net->gram(), net->f(net->sigma_off),
                        net->f(net->scale_off), net->ln_lambda, false, st);
         if (rc) return rc;
     }
-    if (net->n_prep) {   // W / scale and the bf16 planes of every conv, one launch
+    if (net->n_prep && !raw_first) {   // W / scale and the bf16 planes of every conv, one launch
         hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep), dim3(256), 0, st, net->prep(), net->f(net->scale_off),
                            step_begin ? net->loss_acc() : nullptr, net->step());
         LRS_CHECK_LAUNCH();
@@ -1229,6 +1278,15 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
                               wp, (fuse || nq) ? &nsplit : nullptr, act_in_pw ? N.d.act : 0);
             }
             if (rc) return rc;
+            // the raw-weight first conv: its BatchNorm kernel needs the scale (and the GEMM left nsplit
+            // > 1 partials: sn_overlap requires it)
+            const float *sdiv = nullptr;
+            if (raw_first && i == 0) {
+                if (nsplit < 2 || !(nq || fuse)) return LRS_E_INVALID;   // sn_overlap's checks at creation
+                const hipError_t e = hipStreamWaitEvent(st, net->ev_sigma, 0);
+                if (e != hipSuccess) return (int)e;
+                sdiv = net->f(net->scale_off) + N.sn_index;
+            }
             if (act_in_pw) {
                 rc = LRS_OK;
             } else if (nq) {
@@ -1238,17 +1296,23 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
                 const float *pp = nsplit > 1 ? (const float *)net->f(net->part_off) : nullptr;
                 if (bnr_small_wg() && nq == 3 && N.P <= 4 * 256 * 10)
                     hipLaunchKernelGGL((k_bn_fwd_r<10, 256>), dim3(1, N.C), dim3(256), 0, st, pp, nsplit,
-                                       (const float *)(net->params + N.b_off), a);
+                                       (const float *)(net->params + N.b_off), a, sdiv);
                 else
                     LRS_BNR_SWITCH(nq, k_bn_fwd_r, dim3(1, N.C), dim3(kBn1Threads), 0, st, pp, nsplit,
-                                   (const float *)(net->params + N.b_off), a);
+                                   (const float *)(net->params + N.b_off), a, sdiv);
                 rc = LRS_OK;
             } else if (fuse && nsplit > 1) {
                 const BnArgs a{z, out, net->params + N.gm_off, net->params + N.bt_off, net->f(N.mean_off),
                                net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C, nullptr, N.C,
                                (int)N.P, 1, (int)N.P, 1, N.d.act, 1e-5f, 0.1f, lip, 0};
-                hipLaunchKernelGGL(k_reduce_bn1, dim3(1, N.C), dim3(kBn1Threads), 0, st, (const float *)net->f(net->part_off),
-                                   nsplit, (const float *)(net->params + N.b_off), a);
+                if (bn1_threads(N.P) == kBn1Small)
+                    hipLaunchKernelGGL(k_reduce_bn1<kBn1Small>, dim3(1, N.C), dim3(kBn1Small), 0, st,
+                                       (const float *)net->f(net->part_off), nsplit, (const float *)(net->params + N.b_off), a,
+                                       sdiv);
+                else
+                    hipLaunchKernelGGL(k_reduce_bn1<kBn1Threads>, dim3(1, N.C), dim3(kBn1Threads), 0, st,
+                                       (const float *)net->f(net->part_off), nsplit, (const float *)(net->params + N.b_off), a,
+                                       sdiv);
                 rc = LRS_OK;
             } else {
                 rc = bn_fwd(z, out, bn ? net->params + N.gm_off : nullptr, bn ? net->params + N.bt_off : nullptr,
@@ -1301,7 +1365,29 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
     // the weight-preparation launch at the head of the forward also zeroes the loss accumulator
     // and advances Adam's step counter (read only by this step's k_adam); without one, a tiny launch
     const bool folded = net->n_prep > 0;
-    int rc = dipnet_forward(net, x, st, folded);
+    const bool overlap = net->sn_overlap && net->side && net->ev_head && net->ev_sigma;
+    if (overlap) {
+        // the spectral-norm Grams here (alone they take 19 us at 196^2; on the side stream beside the
+        // first conv, 50), then the rest of the chain (Gram reduce, Lanczos) and the preparation of every
+        // conv but the first on the side stream beside the first conv, whose planes come from the raw
+        // weights here
+        // (the Gram reduce too: on the side stream beside the first conv it took 23 us instead of 6)
+        hipLaunchKernelGGL(k_sn_gram_head, dim3(kSnSplit, net->n_sn + 1), dim3(256), 0, st, net->table(), net->gram(),
+                           net->n_sn, (const ConvPrep *)net->prep_head(), net->loss_acc(), net->step());
+        hipLaunchKernelGGL(k_sn_gram_reduce, dim3(kSnPairs, net->n_sn), dim3(256), 0, st, net->table(), net->gram());
+        hipError_t e = hipEventRecord(net->ev_head, st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(net->side, net->ev_head, 0);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(k_sn_sigma, dim3(net->n_sn), dim3(256), 0, net->side, net->table(), net->gram(),
+                           net->f(net->sigma_off), net->f(net->scale_off), net->ln_lambda, (long long *)nullptr);
+        if (net->n_prep_side)
+            hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep_side), dim3(256), 0, net->side,
+                               net->prep_side(), net->f(net->scale_off), (double *)nullptr, net->step());
+        e = hipEventRecord(net->ev_sigma, net->side);
+        if (e != hipSuccess) return (int)e;
+        LRS_CHECK_LAUNCH();
+    }
+    int rc = dipnet_forward(net, x, st, folded, overlap);
     if (rc) return rc;
     const int n = (int)net->nodes.size();
     const auto &Lst = net->nodes[n - 1];
@@ -1417,7 +1503,10 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
                 const BnBwdArgs a{nullptr, outp, z, net->params + N.gm_off, net->f(N.mean_off), net->f(N.istd_off), gz,
                                   net->grads + N.gm_off, net->grads + N.bt_off, net->grads + N.b_off, nullptr, N.C,
                                   (int)N.P, 1, (int)N.P, 1, N.d.act, lip, 0, 0, net->params + N.bt_off};
-                hipLaunchKernelGGL(k_reduce_bn_bwd1, dim3(1, N.C), dim3(kBn1Threads), 0, st, pend, pend_S, a);
+                if (bn1_threads(N.P) == kBn1Small)
+                    hipLaunchKernelGGL(k_reduce_bn_bwd1<kBn1Small>, dim3(1, N.C), dim3(kBn1Small), 0, st, pend, pend_S, a);
+                else
+                    hipLaunchKernelGGL(k_reduce_bn_bwd1<kBn1Threads>, dim3(1, N.C), dim3(kBn1Threads), 0, st, pend, pend_S, a);
                 pend = nullptr;
             } else if (!(head_done && i == n - 1)) {   // else k_mse_head wrote gz and the bias gradient
                 rc = bn_bwd(gout, outp, z, bn ? net->params + N.gm_off : nullptr, net->f(N.mean_off),
@@ -1719,6 +1808,31 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
         if (N.d.kind == LRS_NODE_CONV && (N.sn_index >= 0 || N.wpre_off >= 0)) ++net->n_prep;
     net->prep_off_bytes = (int64_t)bytes;
     bytes += (size_t)round_up((int64_t)((net->n_prep > 0 ? net->n_prep : 1) * sizeof(ConvPrep)), 256);
+    // sigma beside the first conv: a spectrally normalised first conv on the network input whose
+    // BatchNorm kernel finishes its split-K sum (k_bn_fwd_r or k_reduce_bn1, at least 2 partials), read
+    // from weight planes; only where the weight gradients already fork (the side stream exists)
+    {
+        const auto &N0 = net->nodes[0];
+        bool ok = net->fork_w && n_sn > 0 && N0.d.kind == LRS_NODE_CONV && N0.d.in0 == 0 && N0.sn_index >= 0 &&
+                  N0.d.bn && N0.wpre_off >= 0 && !plain_unit(N0.g) && !N0.upc;
+        if (ok) {
+            const bool fuse = N0.P <= 4 * kBn1Threads && bn_split(N0.P) == 1;
+            const bool nq = bn_reg_q(N0.P, N0.P % 4 == 0) > 0;
+            const int kk = N0.g.k * N0.g.k, K = kk * r16(N0.g.Cin);
+            const int S = N0.sm ? sm_split(N0.C, (int)N0.P, K).S
+                                : choose_split(N0.C, (int)N0.P, K, LRS_DIP_SPLIT_BF16, true, fwd_split_target()).S;
+            // only where the first conv is long enough to hide the side chain (~70 us at 196^2: the Gram
+            // reduce, Lanczos and the other convs' planes); at 36^2 the 18^2 first conv takes 7 us and the
+            // overlap measured slower (tuning build: 0.647 -> 0.663 ms per step)
+            ok = (fuse || nq) && S >= 2 && N0.P >= kForkBigP;
+        }
+        net->sn_overlap = ok && tune_knob("LRS_DIP_SN_OVERLAP", 1) != 0;
+    }
+    net->n_prep_side = net->n_prep;
+    net->prep_head_off_bytes = (int64_t)bytes;
+    bytes += 256;   // one ConvPrep
+    net->prep_side_off_bytes = (int64_t)bytes;
+    bytes += (size_t)round_up((int64_t)((net->n_prep > 0 ? net->n_prep : 1) * sizeof(ConvPrep)), 256);
     net->head_fusable = net->nodes.back().d.kind == LRS_NODE_CONV && net->nodes.back().d.bn == 0 &&
                         net->nodes.back().C <= 65535;
     net->headcnt_off_bytes = (int64_t)bytes;   // C per-channel counters + the channel counter
@@ -1738,6 +1852,8 @@ extern "C" void lrs_dipnet_destroy(lrs_dipnet *net) {
     for (hipEvent_t ev : net->ev_fork)
         if (ev) (void)hipEventDestroy(ev);
     if (net->ev_join) (void)hipEventDestroy(net->ev_join);
+    if (net->ev_head) (void)hipEventDestroy(net->ev_head);
+    if (net->ev_sigma) (void)hipEventDestroy(net->ev_sigma);
     for (auto &ps : net->sides) (void)hipStreamDestroy(ps.second);
     delete net;
 }
@@ -1805,6 +1921,22 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
     if (!tab.empty()) e = hipMemcpy(net->table(), tab.data(), sizeof(SnConv) * tab.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && !prep.empty())
         e = hipMemcpy(net->prep(), prep.data(), sizeof(ConvPrep) * prep.size(), hipMemcpyHostToDevice);
+    if (net->sn_overlap && !prep.empty()) {
+        // head: the first conv's forward planes from the raw weights (si = -1: no division, no W / s);
+        // side: every entry, the first conv's without its planes (the main stream reads them meanwhile)
+        ConvPrep head = prep[0], side0 = prep[0];
+        head.Wn = nullptr;
+        head.wd = nullptr;
+        head.si = -1;
+        side0.wf = nullptr;
+        side0.wd = nullptr;
+        std::vector<ConvPrep> side(prep);
+        side[0] = side0;
+        static_assert(sizeof(ConvPrep) <= 256, "one ConvPrep in the head slot");
+        if (e == hipSuccess) e = hipMemcpy(net->prep_head(), &head, sizeof(ConvPrep), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(net->prep_side(), side.data(), sizeof(ConvPrep) * side.size(), hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) e = hipMemset(net->misc_off_bytes + net->ws, 0, 256);
     if (e == hipSuccess) e = hipMemset(net->headcnt(), 0, sizeof(int) * (net->nodes.back().C + 1));
     return e == hipSuccess ? LRS_OK : (int)e;
@@ -1918,6 +2050,8 @@ static int ensure_side(lrs_dipnet *net, hipStream_t st) {
     net->sides.emplace_back(prio, s);
     net->side = s;
     if (!net->ev_join) e = hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming);
+    if (e == hipSuccess && !net->ev_head) e = hipEventCreateWithFlags(&net->ev_head, hipEventDisableTiming);
+    if (e == hipSuccess && !net->ev_sigma) e = hipEventCreateWithFlags(&net->ev_sigma, hipEventDisableTiming);
     for (size_t i = 0; i < net->ev_fork.size() && e == hipSuccess; ++i)
         if (!net->ev_fork[i]) e = hipEventCreateWithFlags(&net->ev_fork[i], hipEventDisableTiming);
     return (int)e;

@@ -33,7 +33,8 @@ run_spec() {   # $1 = tool, $2 = spec
   IFS=',' read -ra kv <<< "$envs"
   for e in "${kv[@]}"; do
     [[ -z $e ]] && continue
-    [[ $e == LRSPNP_LIB=tune ]] && e="LRSPNP_LIB=$T"
+    # LRSPNP_LIB=<v>: the build lrs-pnp-dip_amd/lrspnp/liblrspnp_hip_<v>.so (tune = the tuning build)
+    [[ $e == LRSPNP_LIB=* && $e != LRSPNP_LIB=/* ]] && e="LRSPNP_LIB=$PWD/lrs-pnp-dip_amd/lrspnp/liblrspnp_hip_${e#LRSPNP_LIB=}.so"
     ev+=("$e")
   done
   env "${ev[@]}" timeout -k 10 ${STEP_TIMEOUT:-200} python $tool $args > $O/spec.txt 2>&1 || { tail $O/spec.txt; return 1; }
