@@ -1457,7 +1457,7 @@ bool fork_at(const lrs_dipnet *net, int i) {
         const long v = strtol(p, &e, 10);
         if (e == p) break;
         if (v == i) return true;
-        p = (*e == ',') ? e + 1 : e;
+        p = (*e == ',' || *e == '.') ? e + 1 : e;   // '.' too (tools/gpu.sh specs split on ',')
     }
     return false;
 }
