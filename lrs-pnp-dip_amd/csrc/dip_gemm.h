@@ -150,6 +150,13 @@ __host__ __device__ __forceinline__ int conv_src(int u, int n, int mode, int up)
 }
 
 // ---- implicit-GEMM conv operands --------------------------------------------------------------
+// The tap tables below are built by k_gemm_s3's 256 threads as thread t -> table column t & 127 (the
+// workgroup's pixel), taps t >> 7, t >> 7 + 2, ...: the pixel's coordinates take one division per
+// thread, a tap's (ky, kx) none (k <= 4, the effective 4 x 4 data-gradient kernel included; the
+// per-entry divisions cost ~1.8 us per workgroup).
+__device__ __forceinline__ int s3_tap_y(int kyx, int k) {
+    return kyx >= 3 * k ? 3 : (kyx >= 2 * k ? 2 : (kyx >= k ? 1 : 0));
+}
 // The conv's K index is tap-major, r = kyx * Cp + c (kyx = ky * k + kx, c < Cp = Cin rounded up to
 // 16, channels >= Cin are zero), so the 16 consecutive k a thread loads share one tap: their
 // source offset is one LDS table entry and the 16 channels are a scalar stride apart.  Sources
@@ -169,6 +176,21 @@ __device__ __forceinline__ float s3_bload(__amdgpu_buffer_rsrc_t r, int voff, in
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
+// The NV channel planes c0 .. c0 + NV - 1 (plane stride pb bytes) at one tap's offsets vo, without a
+// branch or a mask: every load is issued, a channel c >= nc reads channel nc - 1.  The values that
+// are not the operand's -- padding channels, and the k groups past a split's end (whose callers
+// read tap 0) -- meet zero weights: every implicit-GEMM B loader is paired with LdPre, whose planes
+// are zero at ci >= Cin (co >= Cout) and which reads zeros past kend, so they add exact zeros.
+// Written as "c < nc ? load : 0" (or with a mask applied to the loaded bits) the compiler branched
+// around each load or waited for it right away, and its wait-count pass, meeting paths with
+// different loads in flight at the GEMM's loop head, drained them all there (s_waitcnt vmcnt(0)
+// every k-step: the prefetch two steps ahead was lost; tools/micro/gemm_phase).
+template <int NV>
+__device__ __forceinline__ void s3_bload_chans(__amdgpu_buffer_rsrc_t r, int vo, int c0, int nc, int pb, float (&v)[NV]) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) v[u] = s3_bload(r, vo, min(c0 + u, nc - 1) * pb);
+}
+
 // Pre-split operand (the conv weights, split into bf16 planes by k_wprep): plane p of row x at
 // P + p * pstride + x * ld, k contiguous.  Loads go straight to the LDS image (no split).
 struct RegP {
@@ -183,14 +205,17 @@ struct LdPre {
     int ld, X;
     int64_t cstride = 0;   // parity-class GEMMs: class cls reads the planes at P + cls * cstride
     __device__ __forceinline__ void setup(int, int *, int cls) { P += cls * cstride; }
+    // buffer loads, branch-free (s3_bload_chans): a row past X or a k group past kend reads at kOob
+    // (zeros); the planes' bytes are < kOob (k_conv_prep's 2^31 / 3 element limit)
     __device__ __forceinline__ void load(int x0, int k0, int kend, RegP &r) const {
         const int x = x0 + s3_row<true>(), kb = k0 + s3_kb<true>();
         const bool ok = x < X && kb < kend;   // K and kend are multiples of 16
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(P, (int)(6 * pstride));
+        const int vo = ok ? 2 * (x * ld + kb) : kOob;
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(P + p * pstride + (int64_t)x * ld + kb);
-            r.h[p][0] = ok ? src[0] : uint4{0, 0, 0, 0};
-            r.h[p][1] = ok ? src[1] : uint4{0, 0, 0, 0};
+            r.h[p][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (int)(2 * p * pstride), 0));
+            r.h[p][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (int)(2 * p * pstride) + 16, 0));
         }
     }
 };
@@ -217,32 +242,22 @@ struct LdFwdTM {
     int *tab;
     __device__ __forceinline__ void setup(int x0, int *smem, int) {
         tab = smem;
-        const int kk = g.k * g.k, P = g.Ho * g.Wo;
-        for (int i = threadIdx.x; i < kk * 128; i += blockDim.x) {
-            const int kyx = i >> 7, p = x0 + (i & 127);
-            int o = kOob;
-            if (p < P) {
-                const int oy = p / g.Wo, ox = p - oy * g.Wo, ky = kyx / g.k, kx = kyx - ky * g.k;
-                const int sy = conv_src(oy * g.stride + ky - g.pad, g.Hu, g.pad_mode, g.up);
-                const int sx = conv_src(ox * g.stride + kx - g.pad, g.Wu, g.pad_mode, g.up);
-                if (sy >= 0 && sx >= 0) o = 4 * (sy * g.Ws + sx);
-            }
-            tab[i] = o;
+        const int kk = g.k * g.k, r = threadIdx.x & 127, p = x0 + r;
+        const bool in = p < g.Ho * g.Wo;
+        const int oy = in ? p / g.Wo : 0, ox = p - oy * g.Wo;
+        for (int kyx = threadIdx.x >> 7; kyx < kk; kyx += 2) {
+            const int ky = s3_tap_y(kyx, g.k), kx = kyx - ky * g.k;
+            const int sy = conv_src(oy * g.stride + ky - g.pad, g.Hu, g.pad_mode, g.up);
+            const int sx = conv_src(ox * g.stride + kx - g.pad, g.Wu, g.pad_mode, g.up);
+            tab[kyx * 128 + r] = (in && sy >= 0 && sx >= 0) ? 4 * (sy * g.Ws + sx) : kOob;
         }
     }
     __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
         const int r0 = __builtin_amdgcn_readfirstlane(k0 + s3_kb<false>());
-        if (r0 >= kend) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = 0.0f;
-            return;
-        }
-        const int kyx = r0 / Cp, c0 = r0 - kyx * Cp;
-        const int pb = g.Hs * g.Ws * 4;
+        const int rr = r0 < kend ? r0 : 0,   // past the chunk: tap 0 (meets zero weights)
+                  kyx = rr / Cp, c0 = rr - kyx * Cp;
         const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
-        const int vo = tab[kyx * 128 + s3_row<false>()];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = c0 + u < g.Cin ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
+        s3_bload_chans(rs, tab[kyx * 128 + s3_row<false>()], c0, g.Cin, g.Hs * g.Ws * 4, v);
     }
 };
 
@@ -258,31 +273,20 @@ struct LdDgradTM {
     int *tab;
     __device__ __forceinline__ void setup(int x0, int *smem, int) {
         tab = smem;
-        const int kk = g.k * g.k, Wp = g.Wu + 2 * g.pad, Q = (g.Hu + 2 * g.pad) * Wp;
-        for (int i = threadIdx.x; i < kk * 128; i += blockDim.x) {
-            const int kyx = i >> 7, q = x0 + (i & 127);
-            int o = kOob;
-            if (q < Q) {
-                const int iy = q / Wp, ix = q - iy * Wp, ky = kyx / g.k, kx = kyx - ky * g.k;
-                const int oy = iy - ky, ox = ix - kx;
-                if (oy >= 0 && oy < g.Ho && ox >= 0 && ox < g.Wo) o = 4 * (oy * g.Wo + ox);
-            }
-            tab[i] = o;
+        const int kk = g.k * g.k, Wp = g.Wu + 2 * g.pad, r = threadIdx.x & 127, q = x0 + r;
+        const bool in = q < (g.Hu + 2 * g.pad) * Wp;
+        const int iy = in ? q / Wp : 0, ix = q - iy * Wp;
+        for (int kyx = threadIdx.x >> 7; kyx < kk; kyx += 2) {
+            const int ky = s3_tap_y(kyx, g.k), kx = kyx - ky * g.k;
+            const int oy = iy - ky, ox = ix - kx;
+            tab[kyx * 128 + r] = (in && oy >= 0 && oy < g.Ho && ox >= 0 && ox < g.Wo) ? 4 * (oy * g.Wo + ox) : kOob;
         }
     }
     __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
         const int r0 = __builtin_amdgcn_readfirstlane(k0 + s3_kb<false>());
-        if (r0 >= kend) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = 0.0f;
-            return;
-        }
-        const int kyx = r0 / Cop, c0 = r0 - kyx * Cop;
-        const int pb = g.Ho * g.Wo * 4;
+        const int rr = r0 < kend ? r0 : 0, kyx = rr / Cop, c0 = rr - kyx * Cop;
         const __amdgpu_buffer_rsrc_t rs = s3_rsrc(GY, gbytes);
-        const int vo = tab[kyx * 128 + s3_row<false>()];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = c0 + u < Cout ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
+        s3_bload_chans(rs, tab[kyx * 128 + s3_row<false>()], c0, Cout, g.Ho * g.Wo * 4, v);
     }
 };
 
@@ -374,30 +378,17 @@ struct LdUpFwdTM {
     int *tab;
     __device__ __forceinline__ void setup(int x0, int *smem, int cls) {
         tab = smem;
-        const int i = cls >> 1, j = cls & 1, Q = g.Hs * g.Ws;
-        for (int idx = threadIdx.x; idx < 4 * 128; idx += blockDim.x) {
-            const int e = idx >> 7, n = x0 + (idx & 127);
-            int o = kOob;
-            if (n < Q) {
-                const int a = n / g.Ws, b = n - a * g.Ws;
-                o = 4 * (clampi(a + (e >> 1) + i - 1, g.Hs) * g.Ws + clampi(b + (e & 1) + j - 1, g.Ws));
-            }
-            tab[idx] = o;
-        }
+        const int i = cls >> 1, j = cls & 1, r = threadIdx.x & 127, n = x0 + r;
+        const bool in = n < g.Hs * g.Ws;
+        const int a = in ? n / g.Ws : 0, b = n - a * g.Ws;
+        for (int e = threadIdx.x >> 7; e < 4; e += 2)
+            tab[e * 128 + r] = in ? 4 * (clampi(a + (e >> 1) + i - 1, g.Hs) * g.Ws + clampi(b + (e & 1) + j - 1, g.Ws)) : kOob;
     }
     __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
         const int r0 = __builtin_amdgcn_readfirstlane(k0 + s3_kb<false>());
-        if (r0 >= kend) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = 0.0f;
-            return;
-        }
-        const int e = r0 / Cp, c0 = r0 - e * Cp;
-        const int pb = g.Hs * g.Ws * 4;
+        const int rr = r0 < kend ? r0 : 0, e = rr / Cp, c0 = rr - e * Cp;
         const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
-        const int vo = tab[e * 128 + s3_row<false>()];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = c0 + u < g.Cin ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
+        s3_bload_chans(rs, tab[e * 128 + s3_row<false>()], c0, g.Cin, g.Hs * g.Ws * 4, v);
     }
 };
 
@@ -415,32 +406,20 @@ struct LdUpDgradTM {
     int *tab;
     __device__ __forceinline__ void setup(int x0, int *smem, int) {
         tab = smem;
-        const int We = g.Ws + 2, Qe = (g.Hs + 2) * We;
-        for (int idx = threadIdx.x; idx < 16 * 128; idx += blockDim.x) {
-            const int ce = idx >> 7, n = x0 + (idx & 127);
-            int o = kOob;
-            if (n < Qe) {
-                const int qy = n / We - 1, qx = n - (qy + 1) * We - 1, cl = ce >> 2, e = ce & 3;
-                const int i = cl >> 1, j = cl & 1;
-                const int a = qy - (e >> 1) - i + 1, b = qx - (e & 1) - j + 1;
-                if (a >= 0 && a < g.Hs && b >= 0 && b < g.Ws) o = 4 * ((2 * a + i) * g.Wo + 2 * b + j);
-            }
-            tab[idx] = o;
+        const int We = g.Ws + 2, r = threadIdx.x & 127, n = x0 + r;
+        const bool in = n < (g.Hs + 2) * We;
+        const int qy = (in ? n / We : 0) - 1, qx = n - (qy + 1) * We - 1;
+        for (int ce = threadIdx.x >> 7; ce < 16; ce += 2) {
+            const int cl = ce >> 2, e = ce & 3, i = cl >> 1, j = cl & 1;
+            const int a = qy - (e >> 1) - i + 1, b = qx - (e & 1) - j + 1;
+            tab[ce * 128 + r] = (in && a >= 0 && a < g.Hs && b >= 0 && b < g.Ws) ? 4 * ((2 * a + i) * g.Wo + 2 * b + j) : kOob;
         }
     }
     __device__ __forceinline__ void load(int, int k0, int kend, float (&v)[16]) const {
         const int r0 = __builtin_amdgcn_readfirstlane(k0 + s3_kb<false>());
-        if (r0 >= kend) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = 0.0f;
-            return;
-        }
-        const int ce = r0 / Cop, c0 = r0 - ce * Cop;
-        const int pb = g.Ho * g.Wo * 4;
+        const int rr = r0 < kend ? r0 : 0, ce = rr / Cop, c0 = rr - ce * Cop;
         const __amdgpu_buffer_rsrc_t rs = s3_rsrc(GY, gbytes);
-        const int vo = tab[ce * 128 + s3_row<false>()];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = c0 + u < Cout ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
+        s3_bload_chans(rs, tab[ce * 128 + s3_row<false>()], c0, Cout, g.Ho * g.Wo * 4, v);
     }
 };
 
@@ -582,6 +561,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
     const int jl = lane & 15, gk = lane >> 4;
     constexpr bool PREP = HasPrepare<LB>::value;
     la.setup(m0, tab, cls);
+    RegP pa;   // LA::pre: the weight planes
+    if constexpr (!PREP && LA::pre) {   // the first weight planes are in flight while the tables are built
+        la.load(m0, kbeg, kend, pa);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     lb.setup(n0, tab, cls);
     if constexpr (PREP) lb.prepare(kbeg, kend, 0);
     __syncthreads();
@@ -591,7 +575,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = s3f4{0.f, 0.f, 0.f, 0.f};
     float va[16], vb[16];
-    RegP pa;   // LA::pre: the weight planes
     static_assert(!LB::pre, "B is never pre-split");
     auto mma = [&]() {
         s3bf8 fb[4][3];
@@ -643,21 +626,29 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
             if constexpr (LanePix<LB>::value) wlp_store(Bs, b);
             else s3_store<LB::kc>(Bs, b);
         };
-        ldA(kbeg);
+        // the prefetches are issued unconditionally (past kend the loaders read zeros or discarded
+        // values without a branch), so every path through the loop has the same loads in flight and the
+        // waits stay counted (s3_bload_chans)
+        // (the A loads of a step are kept ahead of the B loads issued with it: the next step's operands
+        // are then all but the newest 16 loads, a counted wait; reordered, the wait was vmcnt(0))
+        if constexpr (!LA::pre) ldA(kbeg);   // (the weight planes were issued before the tables)
+        __builtin_amdgcn_sched_barrier(0);
         lb.load(n0, kbeg, kend, vb);
-        if (kbeg + kS3K < kend) lb.load(n0, kbeg + kS3K, kend, vb1);
+        lb.load(n0, kbeg + kS3K, kend, vb1);
         for (int k0 = kbeg; k0 < kend; k0 += 2 * kS3K) {
             st(vb);
             __syncthreads();
-            if (k0 + kS3K < kend) ldA(k0 + kS3K);
-            if (k0 + 2 * kS3K < kend) lb.load(n0, k0 + 2 * kS3K, kend, vb);
+            ldA(k0 + kS3K);
+            __builtin_amdgcn_sched_barrier(0);
+            lb.load(n0, k0 + 2 * kS3K, kend, vb);
             mma();
             __syncthreads();
             if (k0 + kS3K >= kend) break;
             st(vb1);
             __syncthreads();
-            if (k0 + 2 * kS3K < kend) ldA(k0 + 2 * kS3K);
-            if (k0 + 3 * kS3K < kend) lb.load(n0, k0 + 3 * kS3K, kend, vb1);
+            ldA(k0 + 2 * kS3K);
+            __builtin_amdgcn_sched_barrier(0);
+            lb.load(n0, k0 + 3 * kS3K, kend, vb1);
             mma();
             __syncthreads();
         }
