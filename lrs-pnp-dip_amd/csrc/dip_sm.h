@@ -113,8 +113,7 @@ struct SmFwd {
         const int pb = g.Hs * g.Ws * 4;
         const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
         const int vo = r0 < kend ? tab[kyx * 64 + sm_row(j)] : kOob;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = c0 + u < g.Cin ? s3_bload(rs, vo, (c0 + u) * pb) : 0.0f;
+        s3_bload_chans(rs, vo, c0, g.Cin, pb, v);   // channels >= Cin meet zero weights (SmPre)
     }
 };
 
@@ -158,21 +157,25 @@ struct SmAdj {
         const __amdgpu_buffer_rsrc_t rs = s3_rsrc(GZ, gbytes);
         int4 o = int4{kOob, kOob, kOob, kOob};
         if (r0 < kend) o = *reinterpret_cast<const int4 *>(tab + 4 * (kyx * 64 + sm_row(j)));
+        // every load issued before any is used (a channel >= Cout reads channel Cout - 1 and meets zero
+        // weights, SmPre): written "c < Cout ? loads : 0", each channel's loads were branched around
+        // and waited for in turn (s_waitcnt vmcnt(0) per channel, tools/micro/gemm_phase's finding)
         if (r0 >= kend || !__builtin_amdgcn_readfirstlane(tab[g.k * g.k * 64 * 4 + kyx])) {   // one term per pixel
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = c0 + u < Cout ? s3_bload(rs, o.x, (c0 + u) * pb) : 0.0f;
+            s3_bload_chans(rs, o.x, c0, Cout, pb, v);
             return;
         }
+        float t[4][8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            float s = 0.0f;
-            if (c0 + u < Cout) {
-                const int so = (c0 + u) * pb;
-                // fixed order (deterministic); terms past the list read kOob = 0
-                s = ((s3_bload(rs, o.x, so) + s3_bload(rs, o.y, so)) + s3_bload(rs, o.z, so)) + s3_bload(rs, o.w, so);
-            }
-            v[u] = s;
+            const int so = min(c0 + u, Cout - 1) * pb;
+            t[0][u] = s3_bload(rs, o.x, so);
+            t[1][u] = s3_bload(rs, o.y, so);
+            t[2][u] = s3_bload(rs, o.z, so);
+            t[3][u] = s3_bload(rs, o.w, so);
         }
+        // fixed order (deterministic); terms past the list read kOob = 0
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ((t[0][u] + t[1][u]) + t[2][u]) + t[3][u];
     }
 };
 
@@ -182,11 +185,12 @@ struct SmDense {
     static constexpr bool pre = false;
     const float *S;
     int ld, X;
+    // buffer loads, the zeros by address (kOob) so no load is branched around (host: X ld 4 < kOob)
     __device__ __forceinline__ void load(int x0, int k0, int kend, int j, float (&v)[8]) const {
         const int x = x0 + sm_row(j), k = k0 + 8 * sm_kg(j);
-        const float *src = S + (int64_t)x * ld + k;
+        const __amdgpu_buffer_rsrc_t rs = s3_rsrc(S, X * ld * 4);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = (x < X && k + u < kend) ? src[u] : 0.0f;
+        for (int u = 0; u < 8; ++u) v[u] = s3_bload(rs, (x < X && k + u < kend) ? 4 * (x * ld + k + u) : kOob, 0);
     }
 };
 
@@ -204,12 +208,13 @@ struct SmWgrad {
         const int c = r / kk, tap = r - c * kk;
         const __amdgpu_buffer_rsrc_t rs = s3_rsrc(X, xbytes);
         const int base = r < Kc ? c * plane : kOob;
+        // the eight table entries in flight together (clamped index, no branch), then the gathers
+        int o[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int p = p0 + u;
-            const int o = p < kend ? tw[tap * P + p] : kOob;
-            v[u] = s3_bload(rs, o == kOob || base == kOob ? kOob : base + o, 0);
-        }
+        for (int u = 0; u < 8; ++u) o[u] = tw[min(tap, kk - 1) * P + min(p0 + u, kend - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v[u] = s3_bload(rs, (p0 + u >= kend || o[u] == kOob || base == kOob) ? kOob : base + o[u], 0);
     }
 };
 
