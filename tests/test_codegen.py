@@ -20,11 +20,12 @@ import yaml
 from lrspnp import _lib
 
 READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 PRODUCT = "_ZN3lrs10k_ista_ln2ILi256ELb0ELi1ELb1ELi1EEEvNS_10IstaParamsE"
 
 
-def kernel_metadata(so):
-    """{kernel name: its amdhsa.kernels metadata} of every gfx950 code object in `so`'s fat binary."""
+def code_objects(so):
+    """The gfx950 code objects (bytes) of `so`'s .hip_fatbin clang offload bundles."""
     sec = subprocess.run([READELF, "-S", "-W", so], capture_output=True, text=True, check=True).stdout
     m = re.search(r"\.hip_fatbin\s+PROGBITS\s+[0-9a-f]+\s+([0-9a-f]+)\s+([0-9a-f]+)", sec)
     assert m, "no .hip_fatbin section"
@@ -32,7 +33,7 @@ def kernel_metadata(so):
     with open(so, "rb") as f:
         f.seek(off)
         data = f.read(size)
-    magic, out, pos = b"__CLANG_OFFLOAD_BUNDLE__", {}, 0
+    magic, out, pos = b"__CLANG_OFFLOAD_BUNDLE__", [], 0
     while (i := data.find(magic, pos)) >= 0:
         n = struct.unpack_from("<Q", data, i + 24)[0]
         p = i + 32
@@ -41,20 +42,66 @@ def kernel_metadata(so):
             p += 24
             triple = data[p:p + tl].decode()
             p += tl
-            if "gfx950" not in triple:
-                continue
-            with tempfile.NamedTemporaryFile(suffix=".co", delete=False) as t:
-                t.write(data[i + eo:i + eo + es])
-            try:
-                notes = subprocess.run([READELF, "--notes", t.name], capture_output=True, text=True, check=True).stdout
-            finally:
-                os.unlink(t.name)
-            doc = notes[notes.index("---"):]
-            doc = doc[:doc.index("\n...")] if "\n..." in doc else doc
-            for k in yaml.safe_load(doc).get("amdhsa.kernels", []):
-                out[k[".name"]] = k
+            if "gfx950" in triple:
+                out.append(data[i + eo:i + eo + es])
         pos = i + 1
     return out
+
+
+def _with_file(co, argv):
+    with tempfile.NamedTemporaryFile(suffix=".co", delete=False) as t:
+        t.write(co)
+    try:
+        return subprocess.run(argv + [t.name], capture_output=True, text=True, check=True).stdout
+    finally:
+        os.unlink(t.name)
+
+
+def kernel_metadata(so):
+    """{kernel name: its amdhsa.kernels metadata} of every gfx950 code object in `so`'s fat binary."""
+    out = {}
+    for co in code_objects(so):
+        notes = _with_file(co, [READELF, "--notes"])
+        doc = notes[notes.index("---"):]
+        doc = doc[:doc.index("\n...")] if "\n..." in doc else doc
+        for k in yaml.safe_load(doc).get("amdhsa.kernels", []):
+            out[k[".name"]] = k
+    return out
+
+
+def mfma_loops(so):
+    """{kernel symbol: [(MFMAs, conditional branches, s_waitcnt vmcnt(0)) per loop that issues MFMAs]}:
+    a loop = the instructions from a backward branch's target to the branch (llvm-objdump)."""
+    res = {}
+    for co in code_objects(so):
+        txt = _with_file(co, [OBJDUMP, "-d", "--mcpu=gfx950"])
+        starts, body, cur = {}, {}, None
+        for line in txt.splitlines():
+            m = re.match(r"^([0-9a-f]+) <(\S+)>:$", line)
+            if m:
+                cur = m.group(2)
+                starts[cur] = int(m.group(1), 16)
+                body[cur] = []
+                continue
+            m = re.search(r"//\s*([0-9A-F]+):", line)
+            if cur and m:
+                body[cur].append((int(m.group(1), 16), line.strip()))
+        for name, ins in body.items():
+            loops = []
+            for k, (a, x) in enumerate(ins):
+                m = re.search(r"s_(?:cbranch_\w+|branch)\s.*<(\S+)\+0x([0-9a-f]+)>", x)
+                if not m or m.group(1) not in starts:
+                    continue
+                tgt = starts[m.group(1)] + int(m.group(2), 16)
+                if tgt >= a:
+                    continue
+                seg = [y for b, y in ins[:k] if b >= tgt]
+                nm = sum("v_mfma" in y for y in seg)
+                if nm:
+                    loops.append((nm, sum("s_cbranch" in y for y in seg), sum("s_waitcnt vmcnt(0)" in y for y in seg)))
+            if loops:
+                res[name] = loops
+    return res
 
 
 @pytest.fixture(scope="module")
@@ -85,3 +132,28 @@ def test_no_scratch_in_hot_kernels(meta):
     bad = [(n, k[".private_segment_fixed_size"]) for n, k in meta.items()
            if k[".private_segment_fixed_size"] > 0 and not any(h in n for h in SCRATCH_OK)]
     assert not bad, bad
+
+
+# The implicit-GEMM conv loops after round 5's branch-free loaders: a loader that wrote
+# "c < Cin ? load : 0" per channel put ~16 conditional branches into every k-loop and, with them, a
+# drain of every load in flight (s_waitcnt vmcnt(0)) at the loop head, which cost the 196^2 step
+# 20 us and the 36^2 step 13 us.  Bounds per MFMA loop: (conditional branches, vmcnt(0) waits).
+LOOP_BOUNDS = {
+    "_ZN3lrs9k_gemm_s3INS_5LdPreENS_7LdFwdTMEEEvNS_8GemmArgsET_T0_": (2, 1),
+    "_ZN3lrs9k_gemm_s3INS_5LdPreENS_9LdDgradTMEEEvNS_8GemmArgsET_T0_": (2, 1),
+    "_ZN3lrs9k_gemm_s3INS_5LdPreENS_9LdUpFwdTMEEEvNS_8GemmArgsET_T0_": (2, 1),
+    "_ZN3lrs9k_gemm_s3INS_5LdPreENS_11LdUpDgradTMEEEvNS_8GemmArgsET_T0_": (2, 1),
+    "_ZN3lrs9k_conv_smINS_5SmFwdENS_5SmPreEEEvNS_8GemmArgsET0_T_": (4, 1),
+    "_ZN3lrs9k_conv_smINS_5SmAdjENS_5SmPreEEEvNS_8GemmArgsET0_T_": (10, 3),
+    "_ZN3lrs9k_conv_smINS_7SmWgradENS_7SmDenseEEEvNS_8GemmArgsET0_T_": (2, 1),
+}
+
+
+def test_conv_loops_keep_their_loads_in_flight():
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump not found")
+    loops = mfma_loops(_lib.LIB_PATH)
+    for name, (br, vm) in LOOP_BOUNDS.items():
+        assert name in loops, f"{name}: no MFMA loop found"
+        for nm, nb, nv in loops[name]:
+            assert nb <= br and nv <= vm, (name, nm, nb, nv)
