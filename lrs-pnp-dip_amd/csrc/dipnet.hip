@@ -16,6 +16,7 @@
 #include "dip_kernels.h"
 #include "dip_gemm.h"
 #include "dip_sm.h"
+#include "dip_dir.h"
 
 using namespace lrs;
 
@@ -1231,6 +1232,15 @@ inline int prep_blocks() {
     return v;
 }
 
+// the largest small map (output pixels) whose conv + BatchNorm run as one k_conv_bn_dir launch:
+// the 9^2 and smaller maps (36^2 step 0.635 -> 0.621 ms; 196^2 within noise; with the 13^2 / 18^2
+// maps too both are slower: 196^2 +28 us, 36^2 +3 us; tuning build, 2 interleaved rounds,
+// profiles/r05/dir/)
+inline int64_t dir_max_p() {
+    static const int64_t v = tune_knob("LRS_DIP_DIR_P", 100);
+    return v;
+}
+
 // raw_first (dipnet_step's overlapped sigma, lrs_dipnet::sn_overlap): the spectral-norm chain and
 // the weight preparation were enqueued by the caller (the first conv's planes from the raw weights on
 // st, the rest on the side stream, which records ev_sigma); the first conv runs on the raw planes and
@@ -1262,6 +1272,28 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
             const int nq = bn ? bn_reg_q(N.P, N.P % 4 == 0 && al16(z) && al16(out) && al16(net->f(net->part_off))) : 0;
             // a 1x1 conv without BN applies its activation in the pointwise kernel's epilogue
             const bool act_in_pw = !bn && plain_unit(N.g) && wp;
+            DirGeom dg;
+            if (bn && N.sm && !N.upc && !(raw_first && i == 0) && N.P <= dir_max_p() && dir_geom(N.g, dg)) {
+                // one launch: direct fp32 conv + BatchNorm (+act), one workgroup per output channel
+                const BnArgs a{z, out, net->params + N.gm_off, net->params + N.bt_off, net->f(N.mean_off),
+                               net->f(N.istd_off), net->bnstats + N.rs_off, net->bnstats + N.rs_off + N.C, nullptr, N.C,
+                               (int)N.P, 1, (int)N.P, 1, N.d.act, 1e-5f, 0.1f, lip, 0};
+                const float *xin = net->tensor(N.d.in0, x), *bias = net->params + N.b_off;
+                const dim3 grid(1, N.C);
+#define LRS_DIR(KS, S)                                                                                           \
+    do {                                                                                                          \
+        if (dg.vec4)                                                                                              \
+            hipLaunchKernelGGL((k_conv_bn_dir<KS, S, true>), grid, dim3(kDirTh), 0, st, xin, w, bias, N.g, dg, a);  \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_conv_bn_dir<KS, S, false>), grid, dim3(kDirTh), 0, st, xin, w, bias, N.g, dg, a); \
+    } while (0)
+                if (N.g.k == 3 && N.g.stride == 1) LRS_DIR(3, 1);
+                else if (N.g.k == 3) LRS_DIR(3, 2);
+                else if (N.g.stride == 1) LRS_DIR(1, 1);
+                else LRS_DIR(1, 2);
+#undef LRS_DIR
+                continue;
+            }
             int nsplit = 1;
             if (N.upc) {   // upsampled 3 x 3: by output parity class
                 rc = upc_fwd(N.g, net->tensor(N.d.in0, x), wp, net->params + N.b_off, N.C, z, net->f(net->part_off),
