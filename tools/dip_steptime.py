@@ -21,11 +21,13 @@ ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--graph", action="store_true")
 ap.add_argument("--net", default="unet", choices=["unet", "skip"], help="the 1-Lip U-Net (configs[2]) or the skip "
                                                                           "net (configs[3])")
+ap.add_argument("--priority", type=int, default=0, help="the net's stream priority (DipNet stream_priority; "
+                                                         "its weight-gradient side stream follows it)")
 ap.add_argument("--dump", default=None, help="also save the net output after the timed rounds (.npy): "
                                               "bit-for-bit A/B of output-preserving kernel changes")
 a = ap.parse_args()
 nodes = lipschitz_unet_nodes(a.bands, a.bands, 128) if a.net == "unet" else skip_nodes(a.bands, a.bands)
-net = DipNet(nodes, a.bands, a.hw, a.hw)
+net = DipNet(nodes, a.bands, a.hw, a.hw, stream_priority=a.priority)
 net.init_params(0)
 g = torch.Generator(device="cuda").manual_seed(0)
 x = torch.rand(a.bands, a.hw, a.hw, device="cuda", generator=g)
