@@ -73,6 +73,13 @@ def parse():
     ap.add_argument("--nit", type=int, default=None)
     ap.add_argument("--K", type=int, default=256)
     ap.add_argument("--dip-steps", type=int, default=100, help="DIP steps per outer iteration (ES off, §8d)")
+    ap.add_argument("--early-stop", action="store_true",
+                    help="the reference's early stopping on (buffer 30, patience 60, at most --dip-cap steps: "
+                         "main_LRS_PnP_DIP_1-LiP.py:221-223,242-264,345): DIP steps vary per outer iteration")
+    ap.add_argument("--dip-cap", type=int, default=5000, help="--early-stop: the step cap (the reference's dip_iter)")
+    ap.add_argument("--data", default="synthetic", choices=["synthetic", "native"],
+                    help="native: the reference's own 36x36x128 image (data_img5: noisy_img5 / clean_img5 + "
+                         "low_rank_sparsity_mask, tests/golden/data_img5.npz), the only real-data size it runs")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--ista-slices", type=int, default=None,
                     help="DIP workloads: launches the sparse coding's Nit is split over (LrsPnPConfig.ista_slices_dip)")
@@ -121,8 +128,12 @@ def ensure_ranks(args):
         sys.exit(2)
 
 
-def make_problem(H, W, B, bb, K, seed, mask="tiled"):
+def make_problem(H, W, B, bb, K, seed, mask="tiled", data="synthetic"):
     from lrspnp.data import load_fixture, mask_matrix, synthetic_cube, synthetic_dictionary, unfold
+    if data == "native":   # the reference mains' own image and mask (tests/test_gpu_e2e_dip.py)
+        d = load_fixture("data_img5.npz")
+        return (unfold(d["noisy"][0]), mask_matrix(d["lrs_mask"], d["noisy"].shape[1]),
+                synthetic_dictionary(bb * bb, K, 0), d["clean"][0])
     base = load_fixture("data_img5.npz")["lrs_mask"] if mask == "tiled" else None
     obs, clean, mask = synthetic_cube(H, W, B, seed=seed, base_mask=base)
     return unfold(obs), mask_matrix(mask, B), synthetic_dictionary(bb * bb, K, 0), clean
@@ -167,10 +178,47 @@ class StreamTimer:
 # ------------------------------------------------------------------------------------------------
 # CPU baseline (oracle), rank 0 at N = 1 only
 # ------------------------------------------------------------------------------------------------
+def host_cpus():
+    """The host's CPUs: nproc (the whole machine), the CPUs this process may run on (affinity), the
+    cgroup's CPU quota (cpu.max, None when unlimited) and the model name (/proc/cpuinfo)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return nproc, aff, quota, model
+
+
 def _threads():
-    t = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    """Threads of the CPU baseline: every CPU this process may use -- the affinity set, bounded by the
+    cgroup quota -- unless OMP_NUM_THREADS fixes the share (the GPU pool sets it to the box's per-GPU
+    CPU share and asks that it be left as it is)."""
+    nproc, aff, quota, _ = host_cpus()
+    avail = min(aff, int(quota)) if quota else aff
+    t = int(os.environ.get("OMP_NUM_THREADS", "0")) or max(1, avail)
     os.environ["OMP_NUM_THREADS"] = str(t)
     return t
+
+
+def host_fields(threads):
+    nproc, aff, quota, model = host_cpus()
+    return {"cores": threads, "nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota, "cpu_model": model,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_sparse_coding(Y, D, bb, nit, variant, budget_s):
@@ -184,8 +232,9 @@ def cpu_sparse_coding(Y, D, bb, nit, variant, budget_s):
     blocks = O.im2col(Y, bb, rows, cols)
     obs = (blocks != 0).astype(np.uint8)
     done, t_alpha, t_ista, batch = 0, 0.0, 0.0, 64 if bb > 8 else 256
+    per_block = []   # seconds per block of each sampled batch (the extrapolation's spread)
     t_start = time.perf_counter()
-    while (time.perf_counter() - t_start < budget_s or done == 0) and done < nb:
+    while (time.perf_counter() - t_start < budget_s or done < 2 * batch) and done < nb:
         idx = rng.choice(nb, batch, replace=False)
         t0 = time.perf_counter()
         al = np.empty(batch, np.float32)
@@ -196,8 +245,11 @@ def cpu_sparse_coding(Y, D, bb, nit, variant, budget_s):
         O.ista_batch(blocks[idx], obs[idx], D, al, th, nit)
         t_ista += time.perf_counter() - t1
         t_alpha += t1 - t0
+        per_block.append((time.perf_counter() - t0) / batch)
         done += batch
-    return (t_alpha + t_ista) / done * nb, done, nb, t_alpha / done * nb
+    pb = np.asarray(per_block)
+    se = float(pb.std(ddof=1) / np.sqrt(pb.size) * nb) if pb.size > 1 else float("nan")
+    return (t_alpha + t_ista) / done * nb, done, nb, t_alpha / done * nb, se
 
 
 def cpu_admm(Y, M, bb):
@@ -216,15 +268,17 @@ def cpu_admm(Y, M, bb):
 def cpu_baseline_pnp(Y, M, D, bb, nit, budget_s):
     from oracle import oracle as O
     threads = _threads()
-    t_sc, done, nb, t_alpha = cpu_sparse_coding(Y, D, bb, nit, "spec2", budget_s * 0.7)
+    t_sc, done, nb, t_alpha, se_sc = cpu_sparse_coding(Y, D, bb, nit, "spec2", budget_s * 0.7)
     t0 = time.perf_counter()
     O.svt(Y, 1 / 0.9)                                       # the reference's float32 LAPACK SVT
     t_svt = time.perf_counter() - t0
     t_admm = cpu_admm(Y, M, bb)
     t_iter = t_sc + t_svt + t_admm
-    return {"value": 1.0 / t_iter, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+    return {"value": 1.0 / t_iter, "unit": "outer_iters/s", **host_fields(threads), "kind": "port",
             # the GPU path computes alpha once per observation pattern, outside the timed steps
             "value_alpha_hoisted": 1.0 / (t_iter - t_alpha),
+            # 95 % interval of the extrapolated time from the spread of the sampled batches
+            "ci95_rel": 1.96 * se_sc / t_iter,
             "sample": f"{done} of {nb} blocks (alpha+ISTA, Nit={nit}) extrapolated x{nb / done:.1f} "
                       f"({t_sc:.1f}s, of which per-block alpha {t_alpha:.1f}s), + full SVT ({t_svt:.2f}s) + "
                       f"full ADMM update ({t_admm:.3f}s); est. {t_iter:.1f}s per outer iteration"}
@@ -236,31 +290,35 @@ def cpu_baseline_dip(solver, Y, M, D, bb, nit, dip_steps, budget_s):
     from oracle import dip_ref
     threads = _threads()
     torch.set_num_threads(threads)
-    t_sc, done, nb, t_alpha = cpu_sparse_coding(Y, D, bb, nit, "fro4", budget_s * 0.4)
+    t_sc, done, nb, t_alpha, se_sc = cpu_sparse_coding(Y, D, bb, nit, "fro4", budget_s * 0.4)
     net = solver.dip.net
     x = solver.dip_in.detach().cpu()
     target = solver.dip_target.detach().cpu()
     mask = solver.dip_mask.detach().cpu()
     tr = dip_ref.RefTrainer(net.nodes, net.params.detach().cpu())
     tr.step(x, target, mask)                                # warm (allocator, thread pool)
-    steps, t_dip = 0, 0.0
+    steps, t_dip, st = 0, 0.0, []
     t_start = time.perf_counter()
-    while time.perf_counter() - t_start < budget_s * 0.5 or steps == 0:
+    while time.perf_counter() - t_start < budget_s * 0.5 or steps < 2:
         t0 = time.perf_counter()
         tr.step(x, target, mask)
-        t_dip += time.perf_counter() - t0
+        st.append(time.perf_counter() - t0)
+        t_dip += st[-1]
         steps += 1
     per_step = t_dip / steps
+    se_dip = float(np.std(st, ddof=1) / np.sqrt(len(st))) * dip_steps
     t_admm = cpu_admm(Y, M, bb)
     t_iter = t_sc + per_step * dip_steps + t_admm
-    return {"value": 1.0 / t_iter, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+    return {"value": 1.0 / t_iter, "unit": "outer_iters/s", **host_fields(threads), "kind": "port",
             # the GPU path computes alpha once per observation pattern, outside the timed steps
             "value_alpha_hoisted": 1.0 / (t_iter - t_alpha),
+            # 95 % interval of the extrapolated time: the sampled batches' and DIP steps' spreads
+            "ci95_rel": 1.96 * float(np.sqrt(se_sc ** 2 + se_dip ** 2)) / t_iter,
             "sample": f"sparse coding: {done} of {nb} blocks (alpha+ISTA, Nit={nit}, oracle C) extrapolated "
                       f"x{nb / done:.1f} = {t_sc:.1f}s (of which per-block alpha {t_alpha:.1f}s, as the reference "
                       f"computes it inside ista; value_alpha_hoisted leaves it out); DIP: {steps} training steps of the torch-CPU restatement "
                       f"(oracle/dip_ref.py: conv/BN/LeakyReLU, full-SVD sigma_max per conv, Adam) at "
-                      f"{per_step:.2f}s/step x {dip_steps} = {per_step * dip_steps:.1f}s; full ADMM update "
+                      f"{per_step:.2f}s/step x {dip_steps:g} = {per_step * dip_steps:.1f}s; full ADMM update "
                       f"{t_admm:.3f}s; est. {t_iter:.1f}s per outer iteration"}
 
 
@@ -315,12 +373,19 @@ def main_dip(args, ctx):
     from lrspnp.dip import DipConfig
     from lrspnp.metrics import mpsnr
     pro = args.workload == "dip-pro"
-    H, W, B = (int(v) for v in args.cube.split("x")) if args.cube else ((512, 512, 224) if pro else (196, 196, 198))
+    native = args.data == "native"
+    if native and args.cube not in (None, "36x36x128"):
+        raise SystemExit("bench.py: --data native is the reference's 36x36x128 image")
+    H, W, B = ((36, 36, 128) if native else (int(v) for v in args.cube.split("x")) if args.cube else
+               ((512, 512, 224) if pro else (196, 196, 198)))
     bb = args.bb or 36
     nit = args.nit or 100
     split = args.split_cube
-    Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=0 if split else ctx.rank, mask=args.mask)
-    dcfg = DipConfig(num_iter=args.dip_steps, early_stop=False, net="skip" if pro else "unet1lip")
+    es = args.early_stop
+    Y, M, Dct, clean = make_problem(H, W, B, bb, args.K, seed=0 if split else ctx.rank, mask=args.mask, data=args.data)
+    # ES off: exactly --dip-steps per outer iteration; ES on: the reference's rule, at most
+    # --dip-cap steps (get_DIP_out, main_LRS_PnP_DIP_1-LiP.py:221-264)
+    dcfg = DipConfig(num_iter=args.dip_cap if es else args.dip_steps, early_stop=es, net="skip" if pro else "unet1lip")
     extra = {} if args.ista_max_wg is None else {"ista_max_wg_dip": args.ista_max_wg}
     if args.ista_slices is not None:
         extra["ista_slices_dip"] = args.ista_slices
@@ -339,9 +404,11 @@ def main_dip(args, ctx):
     orig_alpha, orig_prep = ops.ista_alpha, ops.ista_pat_prepare
     ops.ista_alpha = setup_t.wrap(orig_alpha, lambda a, k: k.get("stream") or torch.cuda.current_stream())
     ops.ista_pat_prepare = setup_t.wrap(orig_prep, lambda a, k: k.get("stream") or torch.cuda.current_stream())
-    task = D.DipTaskSplit(Y, M, Dct, cfg, ctx, image_shape=(H, W)) if split else None
-    s = task.s if split else LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
-    ops.ista_alpha, ops.ista_pat_prepare = orig_alpha, orig_prep
+    try:
+        task = D.DipTaskSplit(Y, M, Dct, cfg, ctx, image_shape=(H, W)) if split else None
+        s = task.s if split else LrsPnP(Y, M, Dct, cfg, image_shape=(H, W))
+    finally:
+        ops.ista_alpha, ops.ista_pat_prepare = orig_alpha, orig_prep
     clean_d = torch.from_numpy(clean).cuda()
     mp0 = mpsnr(s.X, clean_d)
 
@@ -357,8 +424,10 @@ def main_dip(args, ctx):
         count[0] += 1
         (task.step if split else s.step)()
 
-    elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
-    ops.ista, ops.ista_pat = orig_ista, orig_ista_pat
+    try:
+        elapsed = D.timed_steps(step, args.steps, args.warmup, ctx)
+    finally:
+        ops.ista, ops.ista_pat = orig_ista, orig_ista_pat
     setup_ms = setup_t.mean_ms() * len(setup_t.ev)   # (events complete: timed_steps synchronised)
     mp1 = mpsnr(s.X, clean_d)
     # a time-sliced sparse coding (LrsPnPConfig.ista_slices_dip) is several back-to-back launches:
@@ -370,9 +439,13 @@ def main_dip(args, ctx):
         if per is not None:
             dip_ms = per[0][0]
             ista_ms = float(np.nanmean([v[1] for v in per[1:]]))
+    # DIP steps of the timed outer iterations (ES on: to the stop, each different)
+    timed_runs = list(getattr(s, "dip_steps", []))[-args.steps:] if s.dip is not None else []
+    n_dip = float(np.mean([n for n, _ in timed_runs])) if es and timed_runs else float(args.dip_steps)
     # (task-parallel workers build no DIP engine; rank 0, which prints the line, always has one)
-    flops = dip_flops_per_step(s.dip.net) * args.dip_steps if s.dip is not None else float("nan")
-    profiled = not (args.cube or args.bb or args.nit or args.K != 256 or args.dip_steps != 100 or args.mask != "tiled")
+    flops = dip_flops_per_step(s.dip.net) * n_dip if s.dip is not None else float("nan")
+    profiled = not (args.cube or args.bb or args.nit or args.K != 256 or args.dip_steps != 100 or args.mask != "tiled"
+                    or es or native)
     achieved = flops / (dip_ms * 1e-3) / 1e12
     n = bb * bb
     pat = getattr(s, "pat_plan", None) is not None
@@ -387,25 +460,31 @@ def main_dip(args, ctx):
     net_desc = ("skip net (5 x 128 ch, 128-ch skips)" if pro else f"my_Lipschitz_Unet ({B}->128->{B} ch)")
     tag = "dip_pro" if pro else "dip"
     traffic = load_traffic(f"{tag}_hbm_bytes_per_outer_iter", profiled)
-    alg_bytes = dip_alg_bytes_per_step(s.dip.net) * args.dip_steps if s.dip is not None else None
+    alg_bytes = dip_alg_bytes_per_step(s.dip.net) * n_dip if s.dip is not None else None
+    es_desc = (f"ES on (buffer 30, patience 60, cap {args.dip_cap}: {n_dip:.1f} DIP steps per timed outer iteration "
+               f"on average)" if es else "ES off")
+    data_desc = ("the reference's own 36x36x128 image (data_img5 noisy/clean, low_rank_sparsity_mask)" if native else
+                 f"synthetic (seeded low-rank {H}x{W}x{B} cube per rank, "
+                 + ("tiled low_rank_sparsity_mask" if args.mask == "tiled" else
+                    "random mask with 5.1 % missing pixels (no repeated block patterns)") + ")")
     out = {
         "metric": METRIC, "value": (1 if split else ctx.world) * args.steps / elapsed, "unit": "outer_iters/s",
         "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong" if split else "weak",
         "vs_baseline": None, "dtype": "f32 (MFMA products fp32-accurate) + f64 (NLM prox, BN/sigma statistics)",
-        "data": f"synthetic (seeded low-rank {H}x{W}x{B} cube per rank, "
-                + ("tiled low_rank_sparsity_mask" if args.mask == "tiled" else
-                   "random mask with 5.1 % missing pixels (no repeated block patterns)")
-                + f", seeded K={args.K} dictionary, random-init DIP net per outer iteration)",
+        "data": f"{data_desc}, seeded K={args.K} dictionary, random-init DIP net per outer iteration",
         "config": {"workload": (f"LRS-PnP-DIP(pro) skip net on the literal {H}x{W}x{B} cube (BASELINE configs[2] "
                                 f"as written; the skip net maps any H x W)" if pro and (H, W, B) == (200, 200, 198) else
                                 f"LRS-PnP-DIP(pro) {H}x{W}x{B} (BASELINE configs[3]; configs[4] = one such cube per "
                                 f"GPU)" if pro else
+                                f"LRS-PnP-DIP(1-Lip) on the reference's 36x36x128 image" if native else
                                 f"LRS-PnP-DIP(1-Lip) on a {H}x{W}x{B} cube" if args.cube else
                                 f"LRS-PnP-DIP(1-Lip) on the 200x200x198 cube cropped to {H}x{W}x{B} "
                                 f"(BASELINE configs[2]; 196 = largest 16a-12 size <= 200 that the U-Net maps onto "
                                 f"itself)") + f": {bb}x{bb} blocks ({s.nb}), K={args.K}, Nit={nit} fro4 ISTA + NLM "
-                               f"prox; DIP {net_desc} {args.dip_steps} Adam steps per outer iteration, ES off",
+                               f"prox; DIP {net_desc} "
+                               + (f"{args.dip_steps} Adam steps per outer iteration, ES off" if not es else
+                                  f"Adam to the early stop: {es_desc}"),
                    "blocks": s.nb,
                    "mask": args.mask, "observation_patterns": int(s.npat),
                    "sparse_coding_path": "k_ista_pat" if pat else "k_ista_rs",
@@ -414,7 +493,7 @@ def main_dip(args, ctx):
                             "(k_pat_gram + dictionary images): once per solve, outside the timed steps",
                    "parallelism": (f"1 cube, task-parallel: DIP on rank 0, sparse coding over {ctx.world - 1} rank(s)"
                                    if split and ctx.world > 1 else f"{ctx.world} independent cube(s), one per GPU")},
-        "roofline": {"bound": "mfma", "kernel": f"DIP training of one outer iteration ({args.dip_steps} steps: conv "
+        "roofline": {"bound": "mfma", "kernel": f"DIP training of one outer iteration ({n_dip:g} steps: conv "
                                                 f"GEMMs, sigma_max, BN, loss, Adam kernels)",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
@@ -430,8 +509,16 @@ def main_dip(args, ctx):
                                             ista_ms, ista_flops, f"{tag}_ista_hbm_bytes_per_launch", profiled)]},
         "mpsnr": {"input": mp0, "after_steps": mp1, "outer_iterations_run": args.warmup + args.steps},
     }
+    if es:
+        out["early_stopping"] = {
+            "dip_steps_per_outer_iter": [int(n) for n, _ in timed_runs],
+            "stop_epochs": [None if e is None else int(e) for _, e in timed_runs],
+            "mean_dip_steps": n_dip, "s_per_outer_iter": elapsed / args.steps,
+            "dip_ms_per_step": dip_ms / n_dip,
+            "reference": "main_LRS_PnP_DIP_1-LiP.py on its 36x36x128 data, 1st outer iteration: 28.4 s "
+                         "(~165 DIP steps to the stop, 0.127 s per step; BASELINE.md:46)"}
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_dip(s, Y, M, Dct, bb, nit, args.dip_steps, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline_dip(s, Y, M, Dct, bb, nit, n_dip, args.cpu_seconds)
     return out
 
 

@@ -291,6 +291,17 @@ int lrs_bn_act_bwd_f32(const float *gy, const float *y, const float *z, const fl
                        const float *mean, const float *invstd, float *gz, float *ggamma,
                        float *gbeta, float *gbias, int C, int64_t P, int act, void *ws, size_t ws_bytes,
                        void *stream);
+/* Conv -> BatchNorm(train) -> act in one launch on a small map (the network engine's forward for the
+ * <= 9^2 maps): z = conv(reflect_pad(x)) + bias (bias nullable), y = act(BN_lip(z)), mean / invstd
+ * [Cout] saved, running stats (nullable, both or neither) momentum-updated (eps 1e-5, momentum 0.1);
+ * lip = 1: BatchNormSpectralNorm's gamma / c, beta / c.  Replaces a Conv2d + BatchNorm2d +
+ * LeakyReLU block (lipschitz_constraint_layer.py:65-78,88-101, models/common.py:71-121).
+ * LRS_E_UNSUPPORTED where the one-launch kernel does not take the geometry (zero padding, upsample,
+ * a source under 2 x 2, > 1024 output pixels, more than two staged input chunks). */
+int lrs_conv_bn_small_f32(const float *x, int Cin, int H, int W, const float *w, const float *bias, int Cout,
+                          int k, int stride, int pad, int pad_mode, int upsample, const float *gamma,
+                          const float *beta, int lip, int act, float *z, float *y, float *mean, float *invstd,
+                          float *run_mean, float *run_var, void *stream);
 
 /* sigma_max of n weight matrices W[i] (rows[i] x cols[i], min(rows, cols) <= 128; host arrays
  * of device pointers), exact to fp64 before the float32 rounding; scale = max(1, sigma/ln_lambda)

@@ -725,7 +725,8 @@ inline int bn_reg_q(int64_t P, bool vec) {
 // 0.657 ms with 256 threads up to 1024 pixels, but the 196^2 step 1.274 -> 1.280 (its 25^2 maps then
 // hold 3 values per thread).  LRS_DIP_BN1_SMALL = the pixel limit (0: 1024 threads everywhere).
 inline int bn1_threads(int64_t P) {
-    static const int64_t lim = tune_knob("LRS_DIP_BN1_SMALL", 2 * kBn1Small);
+    // (clamped to what a kBn1Small-thread kernel covers: 4 values per thread)
+    static const int64_t lim = std::min<int64_t>(tune_knob("LRS_DIP_BN1_SMALL", 2 * kBn1Small), 4 * kBn1Small);
     return P <= lim ? kBn1Small : kBn1Threads;
 }
 
@@ -1028,6 +1029,39 @@ extern "C" int lrs_bn_act_bwd_f32(const float *gy, const float *y, const float *
     const int rc = bn_ws(ws, ws_bytes, C, P, &part);
     if (rc) return rc;
     return bn_bwd(gy, y, z, gamma, mean, invstd, gz, ggamma, gbeta, gbias, C, P, act, part, (hipStream_t)stream);
+}
+
+// The engine's one-launch small-map conv + BatchNorm (k_conv_bn_dir, dip_dir.h) on its own: the same
+// launch dipnet_forward makes for a conv with BN on a map of <= dir_max_p() pixels.
+extern "C" int lrs_conv_bn_small_f32(const float *x, int Cin, int H, int W, const float *w, const float *bias, int Cout,
+                                     int k, int stride, int pad, int pad_mode, int upsample, const float *gamma,
+                                     const float *beta, int lip, int act, float *z, float *y, float *mean, float *invstd,
+                                     float *run_mean, float *run_var, void *stream) {
+    ConvGeom g;
+    int rc = make_geom(Cin, H, W, k, stride, pad, pad_mode, upsample, g);
+    if (rc) return rc;
+    if (!x || !w || !gamma || !beta || !z || !y || !mean || !invstd || Cout <= 0 || Cout > 65535 ||
+        (!run_mean) != (!run_var) || (lip != 0 && lip != 1))
+        return LRS_E_INVALID;
+    if (act != LRS_ACT_NONE && act != LRS_ACT_LRELU && act != LRS_ACT_SIGMOID) return LRS_E_INVALID;
+    DirGeom dg;
+    if (!dir_geom(g, dg)) return LRS_E_UNSUPPORTED;
+    const int P = g.Ho * g.Wo;
+    const BnArgs a{z, y, gamma, beta, mean, invstd, run_mean, run_var, nullptr, Cout, P, 1, P, 1, act, 1e-5f, 0.1f, lip, 0};
+    const dim3 grid(1, Cout);
+    hipStream_t st = (hipStream_t)stream;
+#define LRS_DIR1(KS, S)                                                                                        \
+    do {                                                                                                        \
+        if (dg.vec4) hipLaunchKernelGGL((k_conv_bn_dir<KS, S, true>), grid, dim3(kDirTh), 0, st, x, w, bias, g, dg, a); \
+        else hipLaunchKernelGGL((k_conv_bn_dir<KS, S, false>), grid, dim3(kDirTh), 0, st, x, w, bias, g, dg, a);     \
+    } while (0)
+    if (g.k == 3 && g.stride == 1) LRS_DIR1(3, 1);
+    else if (g.k == 3) LRS_DIR1(3, 2);
+    else if (g.stride == 1) LRS_DIR1(1, 1);
+    else LRS_DIR1(1, 2);
+#undef LRS_DIR1
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
 }
 
 extern "C" size_t lrs_sigma_max_workspace(int n) {
@@ -1397,7 +1431,10 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
     // the weight-preparation launch at the head of the forward also zeroes the loss accumulator
     // and advances Adam's step counter (read only by this step's k_adam); without one, a tiny launch
     const bool folded = net->n_prep > 0;
-    const bool overlap = net->sn_overlap && net->side && net->ev_head && net->ev_sigma;
+    // (the workspace's 16-B alignment completes the conditions lrs_dipnet_create checked: every
+    // buffer offset is a multiple of 256 B, so the first conv's BatchNorm kernel then takes the
+    // register / fused form the overlap needs, and the forward cannot refuse it mid-step)
+    const bool overlap = net->sn_overlap && net->side && net->ev_head && net->ev_sigma && al16(net->ws);
     if (overlap) {
         // the spectral-norm Grams here (alone they take 19 us at 196^2; on the side stream beside the
         // first conv, 50), then the rest of the chain (Gram reduce, Lanczos) and the preparation of every
@@ -2081,11 +2118,17 @@ static int ensure_side(lrs_dipnet *net, hipStream_t st) {
     if (e != hipSuccess) return (int)e;
     net->sides.emplace_back(prio, s);
     net->side = s;
-    if (!net->ev_join) e = hipEventCreateWithFlags(&net->ev_join, hipEventDisableTiming);
-    if (e == hipSuccess && !net->ev_head) e = hipEventCreateWithFlags(&net->ev_head, hipEventDisableTiming);
-    if (e == hipSuccess && !net->ev_sigma) e = hipEventCreateWithFlags(&net->ev_sigma, hipEventDisableTiming);
+    // The fork / join events only order kernels of this device against each other (nothing on the host
+    // waits on them), so they are recorded with device-scope fences -- what a kernel boundary inside one
+    // stream has -- instead of the default system-scope release, whose cache write-back the critical
+    // stream paid at every fork (tools/micro/fork_cost: DESIGN.md §5).  LRS_DIP_SYSFENCE=1 (tuning
+    // build only) keeps the default events for A/B.
+    static const unsigned evf = hipEventDisableTiming | (tune_knob("LRS_DIP_SYSFENCE", 0) ? 0u : hipEventDisableSystemFence);
+    if (!net->ev_join) e = hipEventCreateWithFlags(&net->ev_join, evf);
+    if (e == hipSuccess && !net->ev_head) e = hipEventCreateWithFlags(&net->ev_head, evf);
+    if (e == hipSuccess && !net->ev_sigma) e = hipEventCreateWithFlags(&net->ev_sigma, evf);
     for (size_t i = 0; i < net->ev_fork.size() && e == hipSuccess; ++i)
-        if (!net->ev_fork[i]) e = hipEventCreateWithFlags(&net->ev_fork[i], hipEventDisableTiming);
+        if (!net->ev_fork[i]) e = hipEventCreateWithFlags(&net->ev_fork[i], evf);
     return (int)e;
 }
 

@@ -114,6 +114,8 @@ def _declare(L):
         "lrs_bn_act_workspace": (sz, [i32, i64]),
         "lrs_bn_act_fwd_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, f32, f32, vp, sz, vp]),
         "lrs_bn_act_bwd_f32": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, i32, vp, sz, vp]),
+        "lrs_conv_bn_small_f32": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32,
+                                        vp, vp, vp, vp, vp, vp, vp]),
         "lrs_sigma_max_workspace": (sz, [i32]),
         "lrs_sigma_max_f32": (i32, [c.POINTER(vp), c.POINTER(vp), c.POINTER(c.c_int), c.POINTER(c.c_int), i32,
                                     f32, vp, vp, vp, sz, vp]),

@@ -15,7 +15,8 @@ import subprocess
 import tempfile
 
 import pytest
-import yaml
+
+yaml = pytest.importorskip("yaml")   # PyYAML reads the code-object notes
 
 from lrspnp import _lib
 

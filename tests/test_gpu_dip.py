@@ -199,6 +199,90 @@ def test_bn_act(L, bn, act, C, HW):
         assert rel(rv, 0.9 + 0.1 * var) < 1e-5 and rel(rm, 0.1 * z.double().mean(1)) < 1e-5
 
 
+# k_conv_bn_dir (dip_dir.h) through lrs_conv_bn_small_f32: every branch dir_geom admits.
+# cin, cout, H, W, k, stride, bias, lip, act
+CONV_BN_DIR_CASES = [
+    (128, 128, 9, 9, 3, 1, True, 1, 1),      # U-Net 9^2 layer: scalar staging (81 % 4 != 0), one chunk
+    (128, 128, 18, 18, 3, 2, True, 1, 1),    # 18^2 -> 9^2: 16-B staging, two chunks (101 + 27 channels)
+    (256, 64, 9, 9, 3, 1, True, 1, 1),       # scalar staging, two chunks (202 + 54)
+    (128, 128, 5, 5, 3, 1, False, 0, 0),     # no bias, plain BatchNorm, no activation
+    (128, 96, 9, 9, 3, 2, True, 0, 1),       # 9^2 -> 5^2, stride 2, scalar staging
+    (200, 16, 3, 3, 3, 1, True, 1, 1),       # 3^2 map: the reflection reaches across the whole map
+    (32, 24, 2, 2, 3, 1, True, 1, 2),        # 2^2 source (the smallest a reflection admits), sigmoid
+    (64, 32, 8, 8, 1, 1, True, 1, 2),        # 1x1, 16-B staging
+    (48, 40, 10, 10, 1, 2, False, 1, 1),     # 1x1 stride 2, 10^2 -> 5^2
+    (16, 8, 24, 12, 3, 2, True, 1, 1),       # non-square, 12 x 6 output
+    (7, 5, 6, 7, 3, 1, True, 1, 1),          # ragged channels, a row of 7 (two strips, one partial)
+]
+
+
+def _conv_bn_ref(x, w, b, gamma, beta, k, stride, lip, act):
+    """fp64 Conv2d(ReflectionPad) -> BatchNorm2d(train) [/ BatchNormSpectralNorm] -> act."""
+    h = x.double()[None]
+    if k == 3:
+        h = F.pad(h, (1, 1, 1, 1), mode="reflect")
+    z = F.conv2d(h, w.double(), None if b is None else b.double(), stride=stride)
+    c = max(float(gamma.abs().max()), 1.0) if lip else 1.0
+    zm = z.mean((0, 2, 3))
+    var = z.var((0, 2, 3), unbiased=False)
+    yb = (z - zm[None, :, None, None]) / torch.sqrt(var + 1e-5)[None, :, None, None]
+    yb = yb * (gamma.double() / c)[None, :, None, None] + (beta.double() / c)[None, :, None, None]
+    y = F.leaky_relu(yb, 0.2) if act == 1 else torch.sigmoid(yb) if act == 2 else yb
+    P = z.shape[2] * z.shape[3]
+    return z[0], y[0], zm, 1.0 / torch.sqrt(var + 1e-5), var * P / max(P - 1, 1)
+
+
+@pytest.mark.parametrize("case", CONV_BN_DIR_CASES)
+def test_conv_bn_small_one_launch(L, case):
+    cin, cout, H, W, k, stride, has_bias, lip, act = case
+    g = torch.Generator().manual_seed(cin * 131 + cout * 7 + H + k + stride)
+    x = torch.randn(cin, H, W, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / np.sqrt(cin * k * k)
+    b = torch.randn(cout, generator=g) * 0.1 if has_bias else None
+    gamma = 0.6 + 0.9 * torch.rand(cout, generator=g)     # max > 1: the Lipschitz rescale acts
+    beta = 0.2 * torch.randn(cout, generator=g)
+    zr, yr, mr, isr, vr = _conv_bn_ref(x, w, b, gamma, beta, k, stride, lip, act)
+    xd, wd, gd, btd = (t.cuda().contiguous() for t in (x, w, gamma, beta))
+    bd = b.cuda() if has_bias else None
+    z = torch.full(zr.shape, float("nan"), device="cuda")
+    y = torch.full(zr.shape, float("nan"), device="cuda")
+    mean, istd = torch.full((cout,), float("nan"), device="cuda"), torch.full((cout,), float("nan"), device="cuda")
+    rm, rv = 0.3 * torch.ones(cout, device="cuda"), 2.0 * torch.ones(cout, device="cuda")
+    rc = L.lrs_conv_bn_small_f32(P(xd), cin, H, W, P(wd), P(bd), cout, k, stride, (k - 1) // 2, 1, 0, P(gd), P(btd),
+                                 lip, act, P(z), P(y), P(mean), P(istd), P(rm), P(rv), S())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert rel(z, zr) < 1e-5
+    assert rel(y, yr) < 1e-5
+    assert rel(mean, mr) < 1e-5
+    assert rel(istd, isr) < 1e-5
+    assert rel(rm, 0.9 * 0.3 + 0.1 * mr) < 1e-5
+    assert rel(rv, 0.9 * 2.0 + 0.1 * vr) < 1e-5
+    # without running statistics: the same outputs, bit for bit
+    z2, y2 = torch.empty_like(z), torch.empty_like(y)
+    m2, i2 = torch.empty_like(mean), torch.empty_like(istd)
+    assert L.lrs_conv_bn_small_f32(P(xd), cin, H, W, P(wd), P(bd), cout, k, stride, (k - 1) // 2, 1, 0, P(gd),
+                                   P(btd), lip, act, P(z2), P(y2), P(m2), P(i2), None, None, S()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(z2, z) and torch.equal(y2, y) and torch.equal(m2, mean) and torch.equal(i2, istd)
+
+
+@pytest.mark.parametrize("cin,H,W,k,stride,pad,pm,up,why", [
+    (16, 9, 9, 3, 1, 1, 0, 0, "zero padding"),
+    (16, 5, 5, 3, 1, 1, 1, 1, "upsample"),
+    (16, 1, 6, 1, 1, 0, 1, 0, "a one-row source"),
+    (8, 40, 40, 1, 1, 0, 1, 0, "1600 output pixels"),
+    (16, 30, 30, 3, 1, 1, 1, 0, "150 row strips (over 64)"),
+    (400, 18, 18, 3, 2, 1, 1, 0, "four staged chunks"),
+    (16, 9, 9, 2, 1, 0, 1, 0, "a 2 x 2 kernel"),
+])
+def test_conv_bn_small_refuses(L, cin, H, W, k, stride, pad, pm, up, why):
+    t = torch.zeros(max(cin * 4 * H * W * 9, 64), device="cuda")
+    c = torch.ones(8, device="cuda")
+    assert L.lrs_conv_bn_small_f32(P(t), cin, H, W, P(t), None, 8, k, stride, pad, pm, up, P(c), P(c), 1, 1,
+                                   P(t), P(t), P(c), P(c), None, None, S()) == -2, why
+
+
 def test_sigma_max(L):
     from lrspnp.dip import sigma_max
     g = torch.Generator().manual_seed(5)

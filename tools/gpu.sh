@@ -2,7 +2,8 @@
 # The one GPU launcher (run on the box through gpurun from the repo root):
 #   tools/gpu.sh suite                 pytest -m gpu, then smoke()
 #   tools/gpu.sh bench [tag]           every bench line (configs[2] default + random mask, configs[3],
-#                                      literal 200^2 skip net, configs[1], native 36^2, torchrun N = 1)
+#                                      literal 200^2 skip net, configs[1], native 36^2 (synthetic and the
+#                                      reference's image), ES-on lines, torchrun N = 1)
 #   tools/gpu.sh steptime SPEC...      DIP step-time A/B: SPEC = label[:ENV=V[,ENV=V...]][@args],
 #                                      interleaved over $ROUNDS rounds (default 2); ENV LRSPNP_LIB=tune
 #                                      selects the tuning build; args go to tools/dip_steptime.py
@@ -62,6 +63,10 @@ bench)
   line dip_pro_200 300 --workload dip-pro --cube 200x200x198 --steps 3 --warmup 1 --no-cpu-baseline
   line pnp 200 --workload pnp --steps 20 --warmup 3 --no-cpu-baseline
   line native36 300 --cube 36x36x128 --steps 20 --warmup 3 --no-cpu-baseline
+  line native36_img 300 --data native --steps 20 --warmup 3 --no-cpu-baseline
+  # early stopping on (the reference's real configuration): DIP steps to the stop per outer iteration
+  line es_native 300 --data native --early-stop --steps 8 --warmup 1 --no-cpu-baseline
+  line es196 600 --early-stop --steps 3 --warmup 1 --no-cpu-baseline
   timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port 29511 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > $O/torchrun_n1.json 2> $O/torchrun_n1.err || { tail -20 $O/torchrun_n1.err; exit 1; }
   python -c "import json; d=json.loads(open('$O/torchrun_n1.json').read().strip().splitlines()[-1]); print('torchrun N=1', d['value'], d['ms_per_step'])"

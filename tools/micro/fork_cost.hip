@@ -6,6 +6,9 @@
 //   mode 2: hipStreamWriteValue32(main) + hipStreamWaitValue32(side)      (stream memory operations)
 //   mode 3: the main-stream kernel itself writes the flag (last workgroup, agent-scope release) and
 //           the side stream waits with hipStreamWaitValue32: no packet on the main stream at all
+//   mode 4: mode 1 with the event created hipEventDisableSystemFence (device-scope fences only: the
+//           consumer is a kernel on the same device)
+//   mode 5: mode 1 with the event created hipEventReleaseToDevice
 // Prints the main-stream time per link; mode k minus mode 0 is the fork's cost to the critical path.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/micro/fork_cost tools/micro/fork_cost.hip
 #include <hip/hip_runtime.h>
@@ -64,13 +67,16 @@ int main(int argc, char **argv) {
     hipStream_t main_s, side;
     CK(hipStreamCreateWithFlags(&main_s, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    hipEvent_t ev, t0, t1;
+    hipEvent_t ev, ev_dev, ev_rel, t0, t1;
     CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&ev_dev, hipEventDisableTiming | hipEventDisableSystemFence));
+    CK(hipEventCreateWithFlags(&ev_rel, hipEventDisableTiming | hipEventReleaseToDevice));
     CK(hipEventCreate(&t0));
     CK(hipEventCreate(&t1));
     unsigned ticket = 0;
     for (int rep = 0; rep < 3; ++rep)
-        for (int mode = 0; mode < 4; ++mode) {
+        for (int mode = 0; mode < 6; ++mode) {
+            if (mode == 3 && argc < 3) continue;   // (345 us per link: measured round 5; argv[2] runs it)
             CK(hipDeviceSynchronize());
             CK(hipEventRecord(t0, main_s));
             for (int i = 0; i < N; ++i) {
@@ -79,9 +85,10 @@ int main(int argc, char **argv) {
                 ++ticket;
                 hipLaunchKernelGGL(k_work, dim3(n / 256), dim3(256), 0, main_s, x, y, n, mode == 3 ? flag : nullptr,
                                    count, ticket);
-                if (mode == 1) {
-                    CK(hipEventRecord(ev, main_s));
-                    CK(hipStreamWaitEvent(side, ev, 0));
+                if (mode == 1 || mode == 4 || mode == 5) {
+                    hipEvent_t e = mode == 1 ? ev : mode == 4 ? ev_dev : ev_rel;
+                    CK(hipEventRecord(e, main_s));
+                    CK(hipStreamWaitEvent(side, e, 0));
                 } else if (mode == 2) {
                     CK(hipStreamWriteValue32(main_s, flag, ticket, 0));
                     CK(hipStreamWaitValue32(side, flag, ticket, hipStreamWaitValueGte, 0xffffffffu));
@@ -96,7 +103,7 @@ int main(int argc, char **argv) {
             float ms;
             CK(hipEventElapsedTime(&ms, t0, t1));
             const char *name[] = {"no fork", "event record + stream wait", "write value + wait value",
-                                  "kernel flag + wait value"};
+                                  "kernel flag + wait value", "event, no system fence", "event, release to device"};
             printf("rep %d mode %d %-28s %8.2f us per link\n", rep, mode, name[mode], 1e3f * ms / N);
         }
     return 0;
