@@ -179,8 +179,8 @@ class StreamTimer:
 # CPU baseline (oracle), rank 0 at N = 1 only
 # ------------------------------------------------------------------------------------------------
 def host_cpus():
-    """The host's CPUs: nproc (the whole machine), the CPUs this process may run on (affinity), the
-    cgroup's CPU quota (cpu.max, None when unlimited) and the model name (/proc/cpuinfo)."""
+    """The host's CPUs: the machine's count, the CPUs this process may run on (affinity), the cgroup's
+    CPU quota (cpu.max, None when unlimited) and the model name (/proc/cpuinfo)."""
     nproc = os.cpu_count() or 1
     try:
         aff = len(os.sched_getaffinity(0))
@@ -215,10 +215,22 @@ def _threads():
     return t
 
 
+def nproc_cmd():
+    """What `nproc` prints here (GNU: the usable CPUs, OMP_NUM_THREADS honoured), None without it."""
+    import shutil
+    exe = shutil.which("nproc")
+    if not exe:
+        return None
+    try:
+        return int(subprocess.run([exe], capture_output=True, text=True, timeout=10).stdout.strip())
+    except (OSError, ValueError, subprocess.SubprocessError):
+        return None
+
+
 def host_fields(threads):
-    nproc, aff, quota, model = host_cpus()
-    return {"cores": threads, "nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota, "cpu_model": model,
-            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+    machine, aff, quota, model = host_cpus()
+    return {"cores": threads, "nproc": nproc_cmd(), "machine_cpus": machine, "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota, "cpu_model": model, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_sparse_coding(Y, D, bb, nit, variant, budget_s):

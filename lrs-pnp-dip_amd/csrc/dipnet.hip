@@ -1893,7 +1893,7 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
             // only where the first conv is long enough to hide the side chain (~70 us at 196^2: the Gram
             // reduce, Lanczos and the other convs' planes); at 36^2 the 18^2 first conv takes 7 us and the
             // overlap measured slower (tuning build: 0.647 -> 0.663 ms per step)
-            ok = (fuse || nq) && S >= 2 && N0.P >= kForkBigP;
+            ok = (fuse || nq) && S >= 2 && N0.P >= tune_knob("LRS_DIP_SN_OVERLAP_MINP", kForkBigP);
         }
         net->sn_overlap = ok && tune_knob("LRS_DIP_SN_OVERLAP", 1) != 0;
     }
