@@ -536,22 +536,34 @@ struct HasPrepare<LdWgradCls> {
 
 constexpr int kS3TabInts = 16 * 128;  // k <= 4 (the 4 x 4 effective kernel of an upsampled 3 x 3 conv's data gradient)
 
+// The LDS of one k_gemm_s3 workgroup: both operand images (one object: the epilogue reuses them as a
+// 4 x 32 x 68-float staging area) and the loaders' tap tables.
+struct S3Smem {
+    struct {
+        S3Tile a, b;
+    } ab;
+    int tab[kS3TabInts];
+};
+static_assert(sizeof(S3Tile) * 2 >= 4 * 32 * 68 * sizeof(float), "epilogue staging fits the operand images");
+
+// One workgroup of the split-bf16 GEMM.  (gx, gy, gz): the GEMM's own grid (N tiles, M tiles, classes x
+// split-K); L: this workgroup's linear index in it.  L must keep the hardware's XCD (L % 8) of the
+// launch's workgroup: k_gemm_s3 passes its own index; k_gemm_s3x2 offsets its second GEMM by a
+// multiple of 8.
 template <class LA, class LB>
-__global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
-    // one object: the epilogue reuses both operand images as a 4 x 32 x 68-float staging area
-    __shared__ __attribute__((aligned(16))) struct { S3Tile a, b; } ab;
-    static_assert(sizeof(ab) >= 4 * 32 * 68 * sizeof(float), "epilogue staging fits the operand images");
+__device__ __forceinline__ void gemm_s3_body(const GemmArgs &g, LA la, LB lb, S3Smem &sm, int L, unsigned gx,
+                                             unsigned gy, unsigned gz) {
+    auto &ab = sm.ab;
     S3Tile &As = ab.a, &Bs = ab.b;
-    __shared__ __attribute__((aligned(16))) int tab[kS3TabInts];
+    int *tab = sm.tab;
     // XCD-aware tile order: the hardware deals workgroup L to XCD L % 8 (placement matters for
     // speed only), so consecutive logical tiles -- neighbouring pixel tiles that share input rows,
     // the N-tiles of one split-K chunk that share its A rows -- are given to one XCD and meet in
     // its L2 instead of being fetched from HBM by all eight
-    const int T = gridDim.x * gridDim.y * gridDim.z;
-    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int T = gx * gy * gz;
     const int xcd = L & 7, q8 = T >> 3, r8 = T & 7;
     const int j = xcd * q8 + min(xcd, r8) + (L >> 3);
-    const int bx = j % gridDim.x, byz = j / gridDim.x, by = byz % gridDim.y, bz = byz / gridDim.y;
+    const int bx = j % gx, byz = j / gx, by = byz % gy, bz = byz / gy;
     const int m0 = by * 128, n0 = bx * 128;
     const int ncls = g.ncls > 1 ? g.ncls : 1, cls = bz % ncls, kz = bz / ncls;   // parity class, split
     const int kbeg = kz * g.kchunk;
@@ -657,7 +669,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
     // stacked classes (cls_wo == 0): output [split][cls][M][N]; else the parity scatter below
     const bool stacked = ncls > 1 && g.cls_wo == 0;
     float *C = g.C + (int64_t)(stacked ? kz * ncls + cls : kz) * g.M * ldc;
-    const bool final_out = (int)gridDim.z == ncls;
+    const bool final_out = (int)gz == ncls;
     const float dv = (final_out && g.div) ? *g.div : 1.0f;
     if (ncls > 1 && !stacked) {
         // parity class: column n = source pixel (a, b) -> output pixel (2a + i, 2b + j)
@@ -743,6 +755,31 @@ __global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
             }
         }
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <class LA, class LB>
+__global__ __launch_bounds__(256, 2) void k_gemm_s3(GemmArgs g, LA la, LB lb) {
+    __shared__ __attribute__((aligned(16))) S3Smem sm;
+    gemm_s3_body(g, la, lb, sm, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gridDim.x, gridDim.y,
+                 gridDim.z);
+}
+
+// Two independent GEMMs in ONE launch (a conv's data gradient and its weight gradient, which read the
+// same dL/dz): a 1-D grid of round_up(T1, 8) + T2 workgroups, the first GEMM's tiles first (they are
+// dispatched first: the data gradient is the critical chain), the padding workgroups leave at once.
+struct S3Grid {
+    unsigned x, y, z;
+};
+template <class LA1, class LB1, class LA2, class LB2>
+__global__ __launch_bounds__(256, 2) void k_gemm_s3x2(GemmArgs g1, LA1 la1, LB1 lb1, S3Grid d1, GemmArgs g2, LA2 la2,
+                                                       LB2 lb2, S3Grid d2) {
+    __shared__ __attribute__((aligned(16))) S3Smem sm;
+    const int T1 = (int)(d1.x * d1.y * d1.z), T1p = (T1 + 7) & ~7, L = blockIdx.x;
+    if (L < T1p) {
+        if (L < T1) gemm_s3_body(g1, la1, lb1, sm, L, d1.x, d1.y, d1.z);
+    } else {
+        gemm_s3_body(g2, la2, lb2, sm, L - T1p, d2.x, d2.y, d2.z);
     }
 }
 

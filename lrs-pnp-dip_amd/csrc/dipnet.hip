@@ -23,7 +23,7 @@ using namespace lrs;
 namespace {
 
 constexpr int kEw = 256;   // elementwise block size
-constexpr int64_t kForkBigP = 9604;   // maps from 98^2 up fork the weight-gradient stream at every conv
+constexpr int64_t kForkBigP = 9604;   // sigma beside the first conv: only where that conv's map is >= 98^2
 
 // A/B tuning knobs.  The environment is read only by the tuning build (make TUNING=1 ->
 // liblrspnp_hip_tune.so, -DLRS_TUNING); the product library always takes the default, so a
@@ -1222,6 +1222,8 @@ struct lrs_dipnet {
     std::vector<hipEvent_t> ev_fork;
     hipEvent_t ev_join = nullptr;
     int64_t part2_off = 0;
+    int64_t part3_off = -1;   // grouped backward (group_bwd): the main stream's weight-gradient partials
+    bool group_bwd = false;   // a conv's data and weight gradients in one launch (k_gemm_s3x2; tuning build)
     // forking pays only when the layers fill the chip (measured: 512^2 skip net 13.0 -> 12.1 ms
     // per step; 196^2 even; 36^2 7-16 % slower from the event overhead)
     bool fork_w = false;
@@ -1531,6 +1533,84 @@ bool fork_at(const lrs_dipnet *net, int i) {
     return false;
 }
 
+// A conv's data gradient and weight gradient as ONE launch (k_gemm_s3x2: the data-gradient tiles
+// first, then the weight-gradient tiles; both read dL/dz), then the fold of the data gradient and the
+// weight gradient's split-K sum, all on stream st: no side-stream fork for this conv.  The stride-1
+// implicit convs (LdDgradTM over the padded domain) and the parity-class upsampled ones.  Returns
+// LRS_E_UNSUPPORTED for a conv it does not take (the caller keeps the two-stream path).
+// Tuning build only (LRS_DIP_GROUP=1): parity-green, but the 196^2 step takes 1.259 ms against 1.189
+// with the side stream (profiles/r06/ab/grouped_backward.txt): the weight gradients'
+// overlap with the folds and BatchNorm kernels is worth more than the forks it saves.
+#ifdef LRS_TUNING
+int group_bwd_conv(lrs_dipnet *net, int i, const float *x, float *gx, int accum_gx, hipStream_t st) {
+    auto &N = net->nodes[i];
+    const ConvGeom &g = N.g;
+    if (N.sm || N.col_off >= 0 || plain_unit(g) || N.wpre_off < 0 || !gx) return LRS_E_UNSUPPORTED;
+    const float *gz = net->f(N.gz_off), *xin = net->tensor(N.d.in0, x);
+    const bool sn = N.sn_index >= 0;
+    const float *wdiv = sn ? net->f(net->scale_off) + N.sn_index : nullptr;
+    float *gw = net->grads + N.w_off, *part = net->f(net->part_off), *part3 = net->f(net->part3_off);
+    float *dcol = net->f(net->dcol_off);
+    const int64_t cap = net->part_cap;
+    const int P = (int)N.P, Cout = N.C, Cop = r16(Cout);
+    if (N.upc) {
+        const int K1 = 16 * Cop, Qe = (g.Hs + 2) * (g.Ws + 2), Q = g.Hs * g.Ws, N2 = 4 * g.Cin;
+        const Split s1 = choose_split(g.Cin, Qe, K1, LRS_DIP_SPLIT_BF16, true, dgrad_split_target());
+        const Split s2 = choose_split(Cout, 4 * N2, Q, LRS_DIP_SPLIT_BF16, true);
+        if ((s1.S > 1 && cap < (int64_t)s1.S * g.Cin * Qe) || cap < (int64_t)s2.S * 4 * Cout * N2) return LRS_E_WORKSPACE;
+        const GemmArgs a1{nullptr, nullptr, s1.S > 1 ? part : dcol, nullptr, nullptr, g.Cin, Qe, K1, s1.kchunk, 0};
+        const GemmArgs a2{nullptr, nullptr, part3, nullptr, nullptr, Cout, N2, Q, s2.kchunk, 0, 4, g.Ws, 0, 0};
+        const S3Grid d1{(unsigned)((Qe + 127) / 128), (unsigned)((g.Cin + 127) / 128), (unsigned)s1.S};
+        const S3Grid d2{(unsigned)((N2 + 127) / 128), (unsigned)((Cout + 127) / 128), (unsigned)(4 * s2.S)};
+        const unsigned nwg = ((d1.x * d1.y * d1.z + 7) & ~7u) + d2.x * d2.y * d2.z;
+        const __bf16 *wd = (const __bf16 *)net->f(N.wpre_off) + wprep_fwd_elems(g, Cout, true);
+        hipLaunchKernelGGL((k_gemm_s3x2<LdPre, LdUpDgradTM, LdGzCls, LdWgradCls>), dim3(nwg), dim3(kGemmThreads), 0, st, a1,
+                           LdPre{wd, (int64_t)g.Cin * K1, K1, g.Cin}, LdUpDgradTM{gz, Cout * g.Ho * g.Wo * 4, g, Cout, Cop, nullptr},
+                           d1, a2, LdGzCls{gz, g.Hs, g.Ws, g.Wo, Cout, 0}, LdWgradCls{xin, g.Cin * Q * 4, g, nullptr, 0, 0}, d2);
+        ConvGeom fg = g;
+        fg.up = 0; fg.Hu = g.Hs; fg.Wu = g.Ws; fg.pad = 1; fg.pad_mode = kPadClamp;
+        hipLaunchKernelGGL(k_fold_pad, dim3((unsigned)((Q + 255) / 256), (unsigned)std::min(g.Cin, 65535)), dim3(256), 0, st,
+                           s1.S > 1 ? part : dcol, s1.S, (int64_t)g.Cin * Qe, fg, gx, accum_gx);
+        const int64_t n = (int64_t)Cout * g.Cin * 9;
+        hipLaunchKernelGGL(k_upc_wgrad_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const float *)part3, s2.S,
+                           Cout, g.Cin, wdiv, gw);
+        LRS_CHECK_LAUNCH();
+        return LRS_OK;
+    }
+    const int kk = g.k * g.k, Qp = (g.Hu + 2 * g.pad) * (g.Wu + 2 * g.pad), Kc = (int)N.Kc;
+    if (g.stride != 1 || up_eff_k(g) || (int64_t)g.Cin * Qp > (int64_t)Kc * P || !conv_implicit_ok(g, Cout))
+        return LRS_E_UNSUPPORTED;
+    const Split s1 = choose_split(g.Cin, Qp, kk * Cop, LRS_DIP_SPLIT_BF16, true, dgrad_split_target());
+    const Split s2 = choose_split(Cout, Kc, P, LRS_DIP_SPLIT_BF16, true);
+    if ((s1.S > 1 && cap < (int64_t)s1.S * g.Cin * Qp) || (s2.S > 1 && cap < (int64_t)s2.S * Cout * Kc))
+        return LRS_E_WORKSPACE;
+    const GemmArgs a1{nullptr, nullptr, s1.S > 1 ? part : dcol, nullptr, nullptr, g.Cin, Qp, kk * Cop, s1.kchunk, 0};
+    const GemmArgs a2{nullptr, nullptr, s2.S > 1 ? part3 : gw, nullptr, wdiv, Cout, Kc, P, s2.kchunk, 0};
+    const S3Grid d1{(unsigned)((Qp + 127) / 128), (unsigned)((g.Cin + 127) / 128), (unsigned)s1.S};
+    const S3Grid d2{(unsigned)((Kc + 127) / 128), (unsigned)((Cout + 127) / 128), (unsigned)s2.S};
+    const unsigned nwg = ((d1.x * d1.y * d1.z + 7) & ~7u) + d2.x * d2.y * d2.z;
+    const __bf16 *wd = (const __bf16 *)net->f(N.wpre_off) + wprep_fwd_elems(g, Cout);
+    hipLaunchKernelGGL((k_gemm_s3x2<LdPre, LdDgradTM, LdDense<true>, LdWgradTM>), dim3(nwg), dim3(kGemmThreads), 0, st, a1,
+                       LdPre{wd, (int64_t)g.Cin * kk * Cop, kk * Cop, g.Cin}, LdDgradTM{gz, Cout * P * 4, g, Cout, Cop, nullptr},
+                       d1, a2, LdDense<true>{gz, P, Cout}, LdWgradTM{xin, g.Cin * g.Hs * g.Ws * 4, g, nullptr, 0}, d2);
+    if (s1.S == 1 && !g.up && g.Ws % 4 == 0 && g.Cin <= 65535 && al16(gx)) {
+        const int q = g.Hs * (g.Ws / 4);
+        hipLaunchKernelGGL(k_fold_pad1q, dim3((unsigned)((q + 255) / 256), (unsigned)g.Cin), dim3(256), 0, st, (const float *)dcol,
+                           g, gx, accum_gx);
+    } else {
+        hipLaunchKernelGGL(k_fold_pad, dim3((unsigned)((g.Hs * g.Ws + 255) / 256), (unsigned)std::min(g.Cin, 65535)), dim3(256), 0,
+                           st, (const float *)(s1.S > 1 ? part : dcol), s1.S, (int64_t)g.Cin * Qp, g, gx, accum_gx);
+    }
+    if (s2.S > 1) {
+        const int64_t MN = (int64_t)Cout * Kc;
+        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((MN + kEw - 1) / kEw)), dim3(kEw), 0, st, (const float *)part3, s2.S,
+                           Cout, Kc, (const float *)nullptr, wdiv, 0, gw);
+    }
+    LRS_CHECK_LAUNCH();
+    return LRS_OK;
+}
+#endif
+
 // pw (lrs_dipnet_train_steps): the input conv's weight gradient may leave its split-K partials for
 // k_adam to finish (AdamPend; pw->part == nullptr when nothing is pending)
 int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done, AdamPend *pw) {
@@ -1590,6 +1670,17 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
             const float *w = sn ? net->f(N.wn_off) : net->params + N.w_off;
             float *gx = t > 0 ? net->f(net->nodes[t - 1].grad_off) : nullptr;
             const float *wdiv = sn ? net->f(net->scale_off) + N.sn_index : nullptr;
+#ifdef LRS_TUNING
+            // grouped (tuning build): data and weight gradient in one launch on this stream
+            if (net->group_bwd && gx) {
+                rc = group_bwd_conv(net, i, x, gx, written[t], st);
+                if (rc == LRS_OK) {
+                    written[t] = 1;
+                    continue;
+                }
+                if (rc != LRS_E_UNSUPPORTED) return rc;
+            }
+#endif
             // weight gradient on the side stream (reads gz, the layer input and the scale only); the
             // nodes between two fork points queue theirs until the next one (fork_at)
             if (net->fork_w && !(t == 0 && i == first_conv)) {
@@ -1835,27 +1926,12 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
         N.grad_off = ofs; ofs += align64((int64_t)N.C * N.P);
         net->nodes.push_back(N);
     }
-    // Fork points: every conv on a map of >= 98^2 pixels; a run of smaller maps forks every second
-    // conv in backward order (and at its end), so the side stream's cheap weight gradients of the
-    // small section go out in pairs.  Each cross-stream fork costs the critical stream time
-    // (tools/micro/event_cost.py); pairs: 196^2 step 1.317 -> 1.305 ms, triples 1.334 (A/B, the
-    // side stream then ends late).
-    {
-        int run = 0;
-        for (int i = (int)net->nodes.size() - 1; i >= 0; --i) {
-            auto &N = net->nodes[i];
-            if (N.d.kind != LRS_NODE_CONV) continue;
-            int prev = i - 1;   // the next conv in backward order
-            while (prev >= 0 && net->nodes[prev].d.kind != LRS_NODE_CONV) --prev;
-            if (N.P >= kForkBigP || prev < 0 || net->nodes[prev].P >= kForkBigP) {
-                N.fork_pt = true;
-                run = 0;
-            } else {
-                N.fork_pt = ++run == 2;
-                if (N.fork_pt) run = 0;
-            }
-        }
-    }
+    // Fork points: every conv forks its weight gradient to the side stream right after its BatchNorm
+    // backward (Node::fork_pt stays true).  Until round 5 a run of small maps forked every second conv
+    // (a fork cost the critical stream ~7 us with system-scope events); with the device-scope events
+    // (ensure_side) forking at every conv is faster at both sizes: 196^2 1.192 -> 1.189 ms, 36^2 0.584
+    // -> 0.580 ms (3 interleaved rounds, profiles/r06/ab/fork_sets.txt).  LRS_DIP_FORK_SET (tuning
+    // build) still picks the fork points for A/B.
     net->n_sn = n_sn;
     net->n_params = pofs;
     net->n_bnstats = rofs;
@@ -1863,6 +1939,10 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     net->dcol_off = ofs; ofs += align64(max_dcol);
     net->part_off = ofs; ofs += align64(part);
     net->part2_off = ofs; ofs += align64(part);
+#ifdef LRS_TUNING
+    net->group_bwd = tune_knob("LRS_DIP_GROUP", 0) != 0;
+#endif
+    if (net->group_bwd) { net->part3_off = ofs; ofs += align64(part); }
     net->part_cap = part;
     net->sigma_off = ofs; ofs += align64(n_sn > 0 ? n_sn : 1);
     net->scale_off = ofs; ofs += align64(n_sn > 0 ? n_sn : 1);

@@ -1,7 +1,7 @@
 """MPSNR trajectory of the ORACLE-driven LRS-PnP-DIP(1-Lip) outer loop on the bench's configs[2]
 cube (run in the BUILD CONTAINER only, ~5 min per seed on 8 cores):
 
-    OMP_NUM_THREADS=8 python tests/golden/gen_dip196_traj.py [seeds] [iters]   # -> dip196_traj_ref.npz
+    OMP_NUM_THREADS=8 python tests/golden/gen_dip196_traj.py [seeds] [iters] [out.npz]   # -> dip196_traj_ref.npz
 
 The reference's main_LRS_PnP_DIP_1-LiP.py cannot run this cube: its my_Lipschitz_Unet hardcodes
 128 bands (models/my_Lipschitz_Unet.py:33-101), and the cube has 198.  So the outer loop is the
@@ -107,7 +107,7 @@ def ista_memo(Yb, OBS, *a, **k):
     return _memo[key]
 
 
-def main(seeds=5, iters=4):
+def main(seeds=5, iters=4, out=OUT):
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "8")))
     O.ista_batch = ista_memo
     Y, M, D, clean = problem()
@@ -127,10 +127,10 @@ def main(seeds=5, iters=4):
         res["seeds"].append(seed)
         res["mpsnr"].append(mp)
         res["loss_last"].append(dip.loss)
-        np.savez(OUT, seeds=np.array(res["seeds"]), mpsnr=np.array(res["mpsnr"]),
+        np.savez(out, seeds=np.array(res["seeds"]), mpsnr=np.array(res["mpsnr"]),
                  loss_last=np.array(res["loss_last"]), mpsnr_input=np.float64(mp0),
                  cube=np.array([H, W, B, BB, 256, 100, DIP_STEPS]))
 
 
 if __name__ == "__main__":
-    main(*(int(a) for a in sys.argv[1:3]))
+    main(*(int(a) for a in sys.argv[1:3]), *(sys.argv[3:4] or [OUT]))
