@@ -326,11 +326,14 @@ int lrs_unfolded_to_image_f32(const float *X, const float *L, float c, int64_t H
 int lrs_image_to_unfolded_f32(const float *img, int64_t H, int64_t W, int64_t B, float *X, void *stream);
 
 /* Early stopping state (device memory).  lrs_es_init fills it; every lrs_es_update_f32 pushes one
- * output into the ring [size][N] and, once full, applies the variance test. */
+ * output into the ring and, once full, applies the variance test.  ring: lrs_es_ring_bytes(size, N)
+ * bytes of device memory -- the last `size` outputs as [size][N] floats (slot = epoch % size), then
+ * the per-pixel window sums the test slides from step to step. */
 typedef struct {
     int32_t count, size, patience, wait, stop, stop_epoch, best_epoch, reserved;
     double best, var_acc, last_var;
 } lrs_es_state;
+size_t lrs_es_ring_bytes(int size, int64_t N);
 int lrs_es_init(lrs_es_state *st, int size, int patience, void *stream);
 int lrs_es_update_f32(const float *out, int64_t N, float *ring, lrs_es_state *st, void *stream);
 

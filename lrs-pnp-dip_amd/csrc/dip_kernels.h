@@ -2008,19 +2008,76 @@ __global__ void k_step_begin(double *loss_acc, int *step) {
 
 // ------------------------------------------------------------------------------------------
 // Early stopping (main_LRS_PnP_DIP_1-LiP.py:71-99, 244-264), on device.
-// ring: [size][N] of the last outputs; slot = (count-1) % size holds the newest.
-// var = mean_i sum_p (ave_p - img_i,p)^2 / N  (myMetric, :102-103), accumulated in fp64.
+// The reference's metric each step, once the last `size` outputs are collected (myMetric, :102-103):
+//   var = mean_j sum_p (ave_p - img_j,p)^2 / N = sum_p (B_p - A_p^2 / size) / (N size),
+// A_p = sum_j img_j,p and B_p = sum_j img_j,p^2 over the ring.  The buffer (lrs_es_ring_bytes) holds the
+// ring [size][N] floats, then A [N] and B [N] (fp64) and the per-workgroup partial sums.  One pass per
+// step (k_es_step) writes the new output into its slot and slides A and B (+ new - the slot's old
+// value: the squares are exact in fp64), so a step reads the ring slot it overwrites and nothing else;
+// every `size` steps (the slot of the last index) A and B are re-summed from the whole ring in slot
+// order, which bounds the sliding sums' rounding drift to `size` updates.  The per-workgroup partials
+// are summed in a fixed order by k_es_decide (deterministic; the round-5 form re-read the whole ring
+// twice per step -- 1.8 GB per step at 196 x 196 x 198 -- and added workgroup sums with atomics).
 // ------------------------------------------------------------------------------------------
-__global__ void k_es_push(const float *__restrict__ out, int64_t N, float *__restrict__ ring, lrs_es_state *st) {
+constexpr int kEsMaxBlocks = 1024;
+
+__host__ __device__ inline int64_t es_ab_offset_bytes(int size, int64_t N) {   // A after the ring, 16-B aligned
+    return ((int64_t)size * N * 4 + 15) / 16 * 16;
+}
+
+__global__ __launch_bounds__(256) void k_es_step(const float *__restrict__ out, int64_t N, float *__restrict__ ring,
+                                                lrs_es_state *st) {
+    __shared__ double red[8];
+    const int S = st->size, c = st->count, slot = c % S;   // c: this output's epoch (k_es_decide increments count)
+    double *A = reinterpret_cast<double *>(reinterpret_cast<char *>(ring) + es_ab_offset_bytes(S, N));
+    double *B = A + N, *part = B + N;
+    float *dst = ring + (int64_t)slot * N;
+    const bool full = c + 1 >= S, refresh = full && slot == S - 1;
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        const float x = out[i];
+        double a, b;
+        if (refresh) {   // the ring in slot order, the new output in the last slot
+            dst[i] = x;
+            a = 0.0;
+            b = 0.0;
+            for (int j = 0; j < S - 1; ++j) {
+                const double v = (double)ring[(int64_t)j * N + i];
+                a += v;
+                b += v * v;
+            }
+            a += (double)x;
+            b += (double)x * (double)x;
+        } else if (c < S) {   // filling: a plain running sum (at c = S - 1 the refresh above)
+            dst[i] = x;
+            a = c == 0 ? (double)x : A[i] + (double)x;
+            b = c == 0 ? (double)x * (double)x : B[i] + (double)x * (double)x;
+        } else {              // sliding: the slot's old output leaves the window
+            const float o = dst[i];
+            dst[i] = x;
+            a = A[i] + ((double)x - (double)o);
+            b = B[i] + ((double)x * (double)x - (double)o * (double)o);
+        }
+        A[i] = a;
+        B[i] = b;
+        if (full) s += b - a * a / (double)S;
+    }
+    s = block_sum_d(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+#ifdef LRS_TUNING
+// The round-5 form (tuning build, LRS_DIP_ES_TWO_PASS=1, A/B only): push, then the whole ring read
+// twice per step (mean, then squared deviations), workgroup sums into var_acc by atomics.
+__global__ void k_es_push_r5(const float *__restrict__ out, int64_t N, float *__restrict__ ring, lrs_es_state *st) {
     const int slot = st->count % st->size;
     float *dst = ring + (int64_t)slot * N;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x)
         dst[i] = out[i];
 }
-
-__global__ void k_es_var(const float *__restrict__ ring, int64_t N, lrs_es_state *st) {
+__global__ void k_es_var_r5(const float *__restrict__ ring, int64_t N, lrs_es_state *st) {
     __shared__ double red[8];
-    if (st->count + 1 < st->size) return;   // count is incremented by k_es_decide
+    if (st->count + 1 < st->size) return;
     const int S = st->size;
     double s = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
@@ -2035,13 +2092,22 @@ __global__ void k_es_var(const float *__restrict__ ring, int64_t N, lrs_es_state
     s = block_sum_d(s, red);
     if (threadIdx.x == 0) atomicAdd(&st->var_acc, s);
 }
+#endif
 
-__global__ void k_es_decide(int64_t N, lrs_es_state *st) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// one wave: the nblk partials of k_es_step in a fixed order, then the reference's patience test
+// (nblk == 0: the round-5 form's var_acc instead)
+__global__ void k_es_decide(const float *ring, int64_t N, int nblk, lrs_es_state *st) {
+    const int S = st->size;
+    const double *part = reinterpret_cast<const double *>(reinterpret_cast<const char *>(ring) + es_ab_offset_bytes(S, N)) + 2 * N;
+    double v = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += 64) v += part[b];
+    v = wave_sum_d(v);   // fixed order
+    if (threadIdx.x != 0) return;
+    if (nblk == 0) v = st->var_acc;
     const int epoch = st->count;           // iteration index i of the reference loop
     st->count += 1;
-    if (st->count >= st->size && !st->stop) {
-        const double var = st->var_acc / (double)N / (double)st->size;
+    if (st->count >= S && !st->stop) {
+        const double var = v / (double)N / (double)S;
         st->last_var = var;
         if (var < st->best) {
             st->best = var;

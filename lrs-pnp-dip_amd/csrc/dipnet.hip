@@ -839,9 +839,19 @@ __global__ void k_es_init(lrs_es_state *st, int size, int patience) {
 }
 
 int es_update(const float *out, int64_t N, float *ring, lrs_es_state *es, hipStream_t st) {
-    hipLaunchKernelGGL(k_es_push, dim3(ew_blocks(N, 1024)), dim3(kEw), 0, st, out, N, ring, es);
-    hipLaunchKernelGGL(k_es_var, dim3(ew_blocks(N, 1024)), dim3(kEw), 0, st, ring, N, es);
-    hipLaunchKernelGGL(k_es_decide, dim3(1), dim3(64), 0, st, N, es);
+    const unsigned nblk = ew_blocks(N, kEsMaxBlocks);
+#ifdef LRS_TUNING
+    static const bool two_pass = tune_knob("LRS_DIP_ES_TWO_PASS", 0) != 0;
+    if (two_pass) {
+        hipLaunchKernelGGL(k_es_push_r5, dim3(nblk), dim3(kEw), 0, st, out, N, ring, es);
+        hipLaunchKernelGGL(k_es_var_r5, dim3(nblk), dim3(kEw), 0, st, (const float *)ring, N, es);
+        hipLaunchKernelGGL(k_es_decide, dim3(1), dim3(64), 0, st, (const float *)ring, N, 0, es);
+        LRS_CHECK_LAUNCH();
+        return LRS_OK;
+    }
+#endif
+    hipLaunchKernelGGL(k_es_step, dim3(nblk), dim3(kEw), 0, st, out, N, ring, es);
+    hipLaunchKernelGGL(k_es_decide, dim3(1), dim3(64), 0, st, (const float *)ring, N, (int)nblk, es);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -1161,6 +1171,11 @@ extern "C" int lrs_es_init(lrs_es_state *st, int size, int patience, void *strea
     return LRS_OK;
 }
 
+extern "C" size_t lrs_es_ring_bytes(int size, int64_t N) {
+    if (size <= 0 || N <= 0) return 0;
+    return (size_t)(es_ab_offset_bytes(size, N) + 2 * N * 8 + kEsMaxBlocks * 8);
+}
+
 extern "C" int lrs_es_update_f32(const float *out, int64_t N, float *ring, lrs_es_state *st, void *stream) {
     if (!out || !ring || !st || N <= 0) return LRS_E_INVALID;
     return es_update(out, N, ring, st, (hipStream_t)stream);
@@ -1205,6 +1220,10 @@ struct lrs_dipnet {
     int n_prep_side = 0;
     int64_t prep_head_off_bytes = 0, prep_side_off_bytes = 0;
     hipEvent_t ev_head = nullptr, ev_sigma = nullptr;
+    // split_ev: ev_sigma right after the Lanczos (the first BatchNorm needs the scale only) and ev_prep
+    // after the other convs' planes (the second conv waits for it); else ev_sigma after both
+    hipEvent_t ev_prep = nullptr;
+    bool split_ev = false;
     int64_t headcnt_off_bytes = 0;   // per-channel counters of k_mse_head (zeroed at bind, reset by the kernel)
     bool head_fusable = false;       // last node = conv without BN: loss + its activation backward in one kernel
     size_t ws_bytes = 0;
@@ -1293,10 +1312,16 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
                            step_begin ? net->loss_acc() : nullptr, net->step());
         LRS_CHECK_LAUNCH();
     }
+    bool prep_waited = !(raw_first && net->split_ev);
     for (size_t i = 0; i < net->nodes.size(); ++i) {
         auto &N = net->nodes[i];
         float *out = net->f(N.out_off);
         const int lip = N.d.bn == 2 ? 1 : 0;
+        if (!prep_waited && i > 0) {   // every later node may read the side stream's planes / W / scale
+            const hipError_t e = hipStreamWaitEvent(st, net->ev_prep, 0);
+            if (e != hipSuccess) return (int)e;
+            prep_waited = true;
+        }
         if (N.d.kind == LRS_NODE_CONV) {
             const bool bn = N.d.bn != 0;
             float *z = bn ? net->f(N.z_off) : out;
@@ -1436,7 +1461,8 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
     // (the workspace's 16-B alignment completes the conditions lrs_dipnet_create checked: every
     // buffer offset is a multiple of 256 B, so the first conv's BatchNorm kernel then takes the
     // register / fused form the overlap needs, and the forward cannot refuse it mid-step)
-    const bool overlap = net->sn_overlap && net->side && net->ev_head && net->ev_sigma && al16(net->ws);
+    const bool overlap = net->sn_overlap && net->side && net->ev_head && net->ev_sigma && (!net->split_ev || net->ev_prep) &&
+                         al16(net->ws);
     if (overlap) {
         // the spectral-norm Grams here (alone they take 19 us at 196^2; on the side stream beside the
         // first conv, 50), then the rest of the chain (Gram reduce, Lanczos) and the preparation of every
@@ -1451,10 +1477,11 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
         if (e != hipSuccess) return (int)e;
         hipLaunchKernelGGL(k_sn_sigma, dim3(net->n_sn), dim3(256), 0, net->side, net->table(), net->gram(),
                            net->f(net->sigma_off), net->f(net->scale_off), net->ln_lambda, (long long *)nullptr);
+        if (net->split_ev && (e = hipEventRecord(net->ev_sigma, net->side)) != hipSuccess) return (int)e;
         if (net->n_prep_side)
             hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep_side), dim3(256), 0, net->side,
                                net->prep_side(), net->f(net->scale_off), (double *)nullptr, net->step());
-        e = hipEventRecord(net->ev_sigma, net->side);
+        e = hipEventRecord(net->split_ev ? net->ev_prep : net->ev_sigma, net->side);
         if (e != hipSuccess) return (int)e;
         LRS_CHECK_LAUNCH();
     }
@@ -1976,6 +2003,7 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
             ok = (fuse || nq) && S >= 2 && N0.P >= tune_knob("LRS_DIP_SN_OVERLAP_MINP", kForkBigP);
         }
         net->sn_overlap = ok && tune_knob("LRS_DIP_SN_OVERLAP", 1) != 0;
+        net->split_ev = net->sn_overlap && tune_knob("LRS_DIP_SPLIT_EV", 0) != 0;
     }
     net->n_prep_side = net->n_prep;
     net->prep_head_off_bytes = (int64_t)bytes;
@@ -2003,6 +2031,7 @@ extern "C" void lrs_dipnet_destroy(lrs_dipnet *net) {
     if (net->ev_join) (void)hipEventDestroy(net->ev_join);
     if (net->ev_head) (void)hipEventDestroy(net->ev_head);
     if (net->ev_sigma) (void)hipEventDestroy(net->ev_sigma);
+    if (net->ev_prep) (void)hipEventDestroy(net->ev_prep);
     for (auto &ps : net->sides) (void)hipStreamDestroy(ps.second);
     delete net;
 }
@@ -2207,6 +2236,7 @@ static int ensure_side(lrs_dipnet *net, hipStream_t st) {
     if (!net->ev_join) e = hipEventCreateWithFlags(&net->ev_join, evf);
     if (e == hipSuccess && !net->ev_head) e = hipEventCreateWithFlags(&net->ev_head, evf);
     if (e == hipSuccess && !net->ev_sigma) e = hipEventCreateWithFlags(&net->ev_sigma, evf);
+    if (e == hipSuccess && !net->ev_prep) e = hipEventCreateWithFlags(&net->ev_prep, evf);
     for (size_t i = 0; i < net->ev_fork.size() && e == hipSuccess; ++i)
         if (!net->ev_fork[i]) e = hipEventCreateWithFlags(&net->ev_fork[i], evf);
     return (int)e;

@@ -124,6 +124,7 @@ def _declare(L):
         "lrs_masked_mse_f32": (i32, [vp, vp, vp, i32, i64, vp, vp, vp]),
         "lrs_unfolded_to_image_f32": (i32, [vp, vp, f32, i64, i64, i64, vp, vp]),
         "lrs_image_to_unfolded_f32": (i32, [vp, i64, i64, i64, vp, vp]),
+        "lrs_es_ring_bytes": (sz, [i32, i64]),
         "lrs_es_init": (i32, [vp, i32, i32, vp]),
         "lrs_es_update_f32": (i32, [vp, i64, vp, vp, vp]),
         "lrs_dipnet_create": (i32, [vp, i32, i32, i32, i32, dop, c.POINTER(vp)]),

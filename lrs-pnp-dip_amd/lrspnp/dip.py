@@ -320,9 +320,10 @@ class EarlyStopper:
         self.size, self.patience, self.n = size, patience, n_elems
         nbytes = ctypes.sizeof(EsState)
         self.state = torch.zeros((nbytes + 7) // 8, dtype=torch.float64, device=device)
-        self.ring = torch.zeros(size * n_elems, dtype=torch.float32, device=device)
-        self._host = None
         L = _lib.device_lib()
+        # the ring [size][N] floats, then the sliding window sums (lrs_es_ring_bytes)
+        self.ring = torch.zeros((L.lrs_es_ring_bytes(size, n_elems) + 3) // 4, dtype=torch.float32, device=device)
+        self._host = None
         _check(L.lrs_es_init(_ptr(self.state), size, patience, None), "lrs_es_init")
 
     def read(self, stream=None) -> EsState:
@@ -337,7 +338,7 @@ class EarlyStopper:
         return EsState.from_buffer_copy(self._host.numpy().tobytes()[:ctypes.sizeof(EsState)])
 
     def slot_of(self, epoch: int):
-        return self.ring.view(self.size, self.n)[epoch % self.size]
+        return self.ring[:self.size * self.n].view(self.size, self.n)[epoch % self.size]
 
 
 @dataclass

@@ -23,6 +23,8 @@ ap.add_argument("--net", default="unet", choices=["unet", "skip"], help="the 1-L
                                                                           "net (configs[3])")
 ap.add_argument("--priority", type=int, default=0, help="the net's stream priority (DipNet stream_priority; "
                                                          "its weight-gradient side stream follows it)")
+ap.add_argument("--es", action="store_true", help="with the device early-stopping update every step (ring 30, "
+                                                   "patience 60), as get_DIP_out runs with early stopping on")
 ap.add_argument("--dump", default=None, help="also save the net output after the timed rounds (.npy): "
                                               "bit-for-bit A/B of output-preserving kernel changes")
 a = ap.parse_args()
@@ -33,13 +35,17 @@ g = torch.Generator(device="cuda").manual_seed(0)
 x = torch.rand(a.bands, a.hw, a.hw, device="cuda", generator=g)
 t = torch.rand(a.bands, a.hw, a.hw, device="cuda", generator=g)
 m = (torch.rand(a.hw, a.hw, device="cuda", generator=g) > 0.2).float()
-net.train_steps(x, t, m, 10, use_graph=a.graph)
+es = None
+if a.es:
+    from lrspnp.dip import EarlyStopper
+    es = EarlyStopper(a.bands * a.hw * a.hw, 30, 10 ** 6)   # never stops: every step runs the full test
+net.train_steps(x, t, m, 10, use_graph=a.graph, es=es)
 torch.cuda.synchronize()
 res = []
 for r in range(a.rounds):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    net.train_steps(x, t, m, a.steps, use_graph=a.graph)
+    net.train_steps(x, t, m, a.steps, use_graph=a.graph, es=es)
     e1.record()
     torch.cuda.synchronize()
     res.append(e0.elapsed_time(e1) / a.steps)
