@@ -64,6 +64,8 @@ CONV_CASES = [
     (64, 32, 10, 7, 3, 1, 1, 0, 1),         # upsampled zero-padded 3x3: effective kernel, no border terms
     (128, 128, 25, 25, 2, 1, 0, 1, 1),      # up_2: effective 3x3 stride-2 data gradient
     (24, 40, 2, 5, 3, 1, 1, 1, 1),          # reflection border on a 2-row source (corners only)
+    (198, 128, 200, 200, 1, 1, 0, 1, 0),    # k_pw, K = 198 over 40,000 pixels: B staged in chunks (128 + 96)
+    (160, 48, 150, 150, 1, 1, 0, 1, 0),     # k_pw, K = 160 in chunks (128 + 32: a partial k-step chunk)
 ]
 
 
