@@ -804,6 +804,13 @@ struct PwArgs {
     int M, Kp32, ldsrow, accum;
     int dbg;   // diagnostics only (LRS_PW_DBG): 1 no C stores, 2 no A loads, 4 no B loads
     int act;   // activation applied after the bias (a conv without BN: its act in the epilogue)
+    // the masked-MSE head fused into the network's last conv (tgt != NULL; k_mse_head's arithmetic per
+    // element): gz = act'(out) * (-norm (tgt m - out m) m) stored beside out, and per output row the
+    // workgroup's fp64 sums of gz and of (tgt m - out m)^2 in hpart[0 / 1][row][blockIdx.x]
+    const float *tgt = nullptr, *msk = nullptr;
+    float *gz = nullptr;
+    double *hpart = nullptr;
+    float hnorm = 0.0f;
 };
 
 inline int pw_ldsrow(int Kp32) {   // bytes; Kp32 * 2 rounded up to 16 mod 256
@@ -943,6 +950,7 @@ __global__ __launch_bounds__(256, 2) void k_pw(PwArgs a) {
     constexpr int ES = NPX + 4;   // staging row stride (floats)
     float *E = reinterpret_cast<float *>(pw_smem) + wv * 16 * ES;
     const bool vec = (a.N & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.C) & 15) == 0);
+    const bool head = a.tgt != nullptr;
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
 #pragma unroll
@@ -951,8 +959,11 @@ __global__ __launch_bounds__(256, 2) void k_pw(PwArgs a) {
             for (int r = 0; r < 4; ++r) E[(4 * gk + r) * ES + 16 * b + jl] = acc[j][b][r];
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done (wave-local tile)
         __builtin_amdgcn_wave_barrier();
+        double hs[NB], hb[NB];   // head: this lane's loss / bias-gradient sums of its run per i
 #pragma unroll
         for (int i = 0; i < NB; ++i) {   // 16 rows x NPX / 4 float4 runs
+            hs[i] = 0.0;
+            hb[i] = 0.0;
             const int idx = lane + 64 * i, rr = idx / (4 * NB), q = 4 * (idx % (4 * NB));
             const int m = 16 * wv + 64 * j + rr;
             const int64_t n = n0 + q;
@@ -968,6 +979,20 @@ __global__ __launch_bounds__(256, 2) void k_pw(PwArgs a) {
                 }
                 if (a.act) { v.x = act_fwd(v.x, a.act); v.y = act_fwd(v.y, a.act); v.z = act_fwd(v.z, a.act); v.w = act_fwd(v.w, a.act); }
                 *reinterpret_cast<float4 *>(c) = v;
+                if (head) {   // k_mse_head's per-element arithmetic, in the same order
+                    const float4 tv = *reinterpret_cast<const float4 *>(a.tgt + (int64_t)m * a.N + n);
+                    const float4 mv = a.msk ? *reinterpret_cast<const float4 *>(a.msk + n) : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+                    const float oe[4] = {v.x, v.y, v.z, v.w}, te[4] = {tv.x, tv.y, tv.z, tv.w}, me[4] = {mv.x, mv.y, mv.z, mv.w};
+                    float ge[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float d = te[e] * me[e] - oe[e] * me[e];
+                        hs[i] += (double)d * (double)d;
+                        ge[e] = act_bwd((-(a.hnorm * d)) * me[e], oe[e], a.act);
+                        hb[i] += (double)ge[e];
+                    }
+                    *reinterpret_cast<float4 *>(a.gz + (int64_t)m * a.N + n) = make_float4(ge[0], ge[1], ge[2], ge[3]);
+                }
             } else {
                 const float vv[4] = {v.x, v.y, v.z, v.w};
                 for (int u = 0; u < 4; ++u) {
@@ -977,11 +1002,65 @@ __global__ __launch_bounds__(256, 2) void k_pw(PwArgs a) {
                     if (a.accum) x = c[u] + x;
                     if (a.act) x = act_fwd(x, a.act);
                     c[u] = x;
+                    if (head) {
+                        const float mk = a.msk ? a.msk[n + u] : 1.0f;
+                        const float d = a.tgt[(int64_t)m * a.N + n + u] * mk - x * mk;
+                        hs[i] += (double)d * (double)d;
+                        const float g = act_bwd((-(a.hnorm * d)) * mk, x, a.act);
+                        a.gz[(int64_t)m * a.N + n + u] = g;
+                        hb[i] += (double)g;
+                    }
                 }
             }
         }
         __builtin_amdgcn_wave_barrier();
+        if (head) {   // each row's sums over the workgroup's runs, in run order, through this wave's LDS
+            double2 *R = reinterpret_cast<double2 *>(E);   // [16 rows x 4 NB runs] (fits the wave's E)
+            static_assert(16 * 4 * NB * sizeof(double2) <= 16 * ES * sizeof(float), "head sums fit the staging");
+#pragma unroll
+            for (int i = 0; i < NB; ++i) R[lane + 64 * i] = make_double2(hs[i], hb[i]);
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            const int m = 16 * wv + 64 * j + lane;
+            if (lane < 16 && m < a.M) {
+                double sl = 0.0, sg = 0.0;
+                for (int k = 0; k < 4 * NB; ++k) {
+                    const double2 p = R[lane * 4 * NB + k];
+                    sl += p.x;
+                    sg += p.y;
+                }
+                a.hpart[(int64_t)m * gridDim.x + blockIdx.x] = sg;
+                a.hpart[((int64_t)a.M + m) * gridDim.x + blockIdx.x] = sl;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
     }
+}
+
+// The fused head's sums (k_pw with PwArgs::tgt): per channel c (grid C) the gz sums of the nwg
+// workgroups, summed in a fixed order -> the conv's bias gradient, and the loss sums -> closs[c];
+// k_head_loss then adds closs in channel order into loss_acc (deterministic, as k_mse_head).
+__global__ __launch_bounds__(256) void k_head_reduce(const double *__restrict__ hpart, int C, int nwg, float *gbias,
+                                                     double *closs) {
+    __shared__ double red[12];
+    const int c = blockIdx.x;
+    double sg = 0.0, sl = 0.0;
+    for (int w = threadIdx.x; w < nwg; w += blockDim.x) {
+        sg += hpart[(int64_t)c * nwg + w];
+        sl += hpart[((int64_t)C + c) * nwg + w];
+    }
+    block_sum2_d(sg, sl, red);
+    if (threadIdx.x == 0) {
+        gbias[c] = (float)sg;
+        closs[c] = sl;
+    }
+}
+
+__global__ void k_head_loss(const double *__restrict__ closs, int C, double *loss_acc) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double s = 0.0;
+    for (int c = 0; c < C; ++c) s += closs[c];
+    *loss_acc += s;
 }
 
 // Per-step weight preparation of every conv of a network in ONE launch (grid (blocks, convs)):

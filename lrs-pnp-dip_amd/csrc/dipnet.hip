@@ -540,8 +540,16 @@ static const PwKernel kPwKernels[] = {
 // 3 x 16 NB x ldsrow bytes and the registers both limit them) times the per-workgroup work (NB),
 // wider on ties.  At 196^2 the 198-row last 1x1 runs on 80 pixels: 481 workgroups, one round of
 // 2 per CU instead of 1.2 rounds at 64 (A/B: -10 us per step).
+struct PwHead {   // the fused masked-MSE head of a network's last conv (PwArgs::tgt)
+    const float *tgt, *msk;
+    float *gz;
+    double *hpart;
+    float norm;
+    int *nwg_out;   // the grid the launch used (k_head_reduce's partial count)
+};
+
 int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, int K, int64_t N, float *C,
-              const float *bias, int accum, hipStream_t st, int act = 0) {
+              const float *bias, int accum, hipStream_t st, int act = 0, const PwHead *head = nullptr) {
     if (M <= 0 || N <= 0) return LRS_OK;
     if (M > 256 || lda < K || lda % 16) return LRS_E_UNSUPPORTED;
     const int Kp32 = (int)round_up(lda, 32), ldsrow = pw_ldsrow(Kp32);
@@ -568,7 +576,16 @@ int pw_launch(const __bf16 *A, int64_t pstride, int lda, int M, const float *B, 
     }
     if (!best) return LRS_E_UNSUPPORTED;
     const int npx = 16 * best->nb;
-    hipLaunchKernelGGL(best->fn, dim3((unsigned)((N + npx - 1) / npx)), dim3(256), 3 * npx * ldsrow, st, a);
+    PwArgs ah = a;
+    if (head) {
+        ah.tgt = head->tgt;
+        ah.msk = head->msk;
+        ah.gz = head->gz;
+        ah.hpart = head->hpart;
+        ah.hnorm = head->norm;
+        *head->nwg_out = (int)((N + npx - 1) / npx);
+    }
+    hipLaunchKernelGGL(best->fn, dim3((unsigned)((N + npx - 1) / npx)), dim3(256), 3 * npx * ldsrow, st, ah);
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -580,12 +597,13 @@ inline bool pw_ok(const ConvGeom &g, int Cout) { return plain_unit(g) && Cout <=
 // act_pw: activation for the pointwise kernel's epilogue (a 1x1 conv without BN), applied only there.
 int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bias, int Cout, float *col, float *y,
              float *part, int64_t part_cap, hipStream_t st, const __bf16 *wpre = nullptr, int *nsplit_out = nullptr,
-             int act_pw = 0) {
+             int act_pw = 0, const PwHead *head = nullptr) {
     const int P = g.Ho * g.Wo, Kc = g.Cin * g.k * g.k;
     if (nsplit_out) *nsplit_out = 1;
     const float *B = x;
     if (plain_unit(g) && wpre)      // 1x1: pointwise kernel on the pre-split weights
-        return pw_launch(wpre, (int64_t)Cout * r16(g.Cin), r16(g.Cin), Cout, x, g.Cin, P, y, bias, 0, st, act_pw);
+        return pw_launch(wpre, (int64_t)Cout * r16(g.Cin), r16(g.Cin), Cout, x, g.Cin, P, y, bias, 0, st, act_pw, head);
+    if (head) return LRS_E_UNSUPPORTED;
     if (!plain_unit(g) && !col) {   // implicit im2col
         if (!conv_implicit_ok(g, Cout) || !wpre) return LRS_E_UNSUPPORTED;
         const int kk = g.k * g.k, Cp = r16(g.Cin);
@@ -623,7 +641,8 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         // kernel (A/B in the 196^2 training step, configs[2]: 5.50 -> 5.65 outer it/s against the f32
         // 64-tile kernel; alone the two are within 12 %, but the f32 kernel's 512 workgroups hold the
         // CUs the concurrent data-gradient chain needs for longer)
-        rc = gemm(g.prec, 0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st, 0, nullptr, plain_unit(g));
+        // (wsplit_out: as above, the caller's k_adam finishes the split-K sum)
+        rc = gemm(g.prec, 0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st, 0, wsplit_out, plain_unit(g));
     }
     if (rc || !gx) return rc;
     if (plain_unit(g) && wpre)      // 1x1 data gradient: W^T planes (wprep's WD)
@@ -1226,6 +1245,11 @@ struct lrs_dipnet {
     bool split_ev = false;
     int64_t headcnt_off_bytes = 0;   // per-channel counters of k_mse_head (zeroed at bind, reset by the kernel)
     bool head_fusable = false;       // last node = conv without BN: loss + its activation backward in one kernel
+    // ... and when that conv is a 1x1 on k_pw, the loss head runs in the conv's own epilogue (PwHead);
+    // its per-workgroup sums go to hpart, reduced by k_head_reduce / k_head_loss on the side stream
+    bool head_pw = false;
+    int head_nwg = 0;
+    int64_t hpart_off_bytes = 0, closs_off_bytes = 0;
     size_t ws_bytes = 0;
     int n_sn = 0;
     int64_t max_w = 0;
@@ -1264,6 +1288,8 @@ struct lrs_dipnet {
     double *loss_acc() const { return (double *)(ws + misc_off_bytes); }
     int *step() const { return (int *)(ws + misc_off_bytes + 8); }
     double *bnpart() const { return (double *)(ws + bnpart_off_bytes); }
+    double *hpart() const { return (double *)(ws + hpart_off_bytes); }
+    double *closs() const { return (double *)(ws + closs_off_bytes); }
     const float *tensor(int t, const float *x) const { return t == 0 ? x : f(nodes[t - 1].out_off); }
     int tC(int t) const { return t == 0 ? C0 : nodes[t - 1].C; }
     int tH(int t) const { return t == 0 ? H : nodes[t - 1].H; }
@@ -1300,7 +1326,8 @@ inline int64_t dir_max_p() {
 // the weight preparation were enqueued by the caller (the first conv's planes from the raw weights on
 // st, the rest on the side stream, which records ev_sigma); the first conv runs on the raw planes and
 // st waits for ev_sigma before its BatchNorm kernel, which divides by the scale.
-int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_begin = false, bool raw_first = false) {
+int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_begin = false, bool raw_first = false,
+                   const PwHead *head = nullptr) {
     int rc;
     if (net->n_sn && !raw_first) {
         rc = sn_launch(net->table(), net->n_sn, net->max_w, net->gram(), net->f(net->sigma_off),
@@ -1368,7 +1395,8 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
             } else {
                 rc = conv_fwd(N.g, net->tensor(N.d.in0, x), w, net->params + N.b_off, N.C,
                               N.col_off >= 0 ? net->f(N.col_off) : nullptr, z, net->f(net->part_off), net->part_cap, st,
-                              wp, (fuse || nq) ? &nsplit : nullptr, act_in_pw ? N.d.act : 0);
+                              wp, (fuse || nq) ? &nsplit : nullptr, act_in_pw ? N.d.act : 0,
+                              (head && i + 1 == net->nodes.size() && act_in_pw) ? head : nullptr);
             }
             if (rc) return rc;
             // the raw-weight first conv: its BatchNorm kernel needs the scale (and the GEMM left nsplit
@@ -1430,7 +1458,8 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
     return LRS_OK;
 }
 
-int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done = false, AdamPend *pw = nullptr);
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done = false, AdamPend *pw = nullptr,
+                    bool head_reduce = false);
 int mse_head(lrs_dipnet *net, const float *out, const float *target, const float *mask, hipStream_t st);
 
 // k_mse_head over the last node (conv without BN): gz and the bias gradient of that node, + loss
@@ -1485,13 +1514,20 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
         if (e != hipSuccess) return (int)e;
         LRS_CHECK_LAUNCH();
     }
-    int rc = dipnet_forward(net, x, st, folded, overlap);
-    if (rc) return rc;
     const int n = (int)net->nodes.size();
     const auto &Lst = net->nodes[n - 1];
+    // the loss head in the last conv's epilogue (k_pw): gz, and per-workgroup sums for the bias gradient
+    // and the loss, reduced in the backward on the side stream (k_mse_head's arithmetic per element)
+    const PwHead hd{target, mask, net->f(Lst.gz_off), net->hpart(), (float)(2.0 / ((double)Lst.C * (double)Lst.P)),
+                    &net->head_nwg};
+    const bool fused_head = net->head_pw && (!mask || al16(mask)) && al16(target);
+    int rc = dipnet_forward(net, x, st, folded, overlap, fused_head ? &hd : nullptr);
+    if (rc) return rc;
     const float *out = net->f(Lst.out_off);
     if (!folded) hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, st, net->loss_acc(), net->step());
-    if (net->head_fusable) {
+    if (fused_head) {
+        rc = LRS_OK;
+    } else if (net->head_fusable) {
         rc = mse_head(net, out, target, mask, st);
     } else {
         rc = lrs_masked_mse_f32(out, target, mask, Lst.C, Lst.P, net->f(Lst.grad_off), net->loss_acc(), st);
@@ -1500,7 +1536,7 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
     // the input conv's weight-gradient split-K sum is finished inside Adam (one launch less on the
     // step's tail)
     AdamPend pw{};
-    rc = dipnet_backward(net, x, st, net->head_fusable, &pw);
+    rc = dipnet_backward(net, x, st, net->head_fusable, &pw, fused_head);
     if (rc) return rc;
     hipLaunchKernelGGL(k_adam, dim3(ew_blocks((net->n_params + 3) / 4, 8192)), dim3(kEw), 0, st, net->params,
                        (const float *)net->grads, net->am, net->av, net->n_params, (const int *)net->step(), lr, b1, b2,
@@ -1640,9 +1676,20 @@ int group_bwd_conv(lrs_dipnet *net, int i, const float *x, float *gx, int accum_
 
 // pw (lrs_dipnet_train_steps): the input conv's weight gradient may leave its split-K partials for
 // k_adam to finish (AdamPend; pw->part == nullptr when nothing is pending)
-int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done, AdamPend *pw) {
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done, AdamPend *pw, bool head_reduce) {
     int rc;
     const int n = (int)net->nodes.size();
+    // the fused loss head's sums (PwHead): the bias gradient of the last conv (read by Adam only) and the
+    // loss, on the side stream with the first weight gradients (or here, without a side stream)
+    auto head_sums = [&](hipStream_t hs) {
+        if (!head_reduce) return;
+        const auto &Lh = net->nodes[n - 1];
+        hipLaunchKernelGGL(k_head_reduce, dim3((unsigned)Lh.C), dim3(256), 0, hs, (const double *)net->hpart(), Lh.C,
+                           net->head_nwg, net->grads + Lh.b_off, net->closs());
+        hipLaunchKernelGGL(k_head_loss, dim3(1), dim3(64), 0, hs, (const double *)net->closs(), Lh.C, net->loss_acc());
+        head_reduce = false;
+    };
+    if (!net->fork_w) head_sums(st);
     // gradient buffers: the first contribution to a tensor writes, later ones accumulate
     std::vector<char> written(n + 1, 0);
     written[n] = 1;
@@ -1656,6 +1703,7 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
         hipError_t e = hipEventRecord(net->ev_fork[j], st);
         if (e == hipSuccess) e = hipStreamWaitEvent(net->side, net->ev_fork[j], 0);
         if (e != hipSuccess) return (int)e;
+        head_sums(net->side);
         for (int q : wq)
             if (const int r = weight_grad(net, q, x, net->side, net->f(net->part2_off))) return r;
         wq.clear();
@@ -1805,6 +1853,7 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
         if (e == hipSuccess) e = hipStreamWaitEvent(st, net->ev_join, 0);
         if (e != hipSuccess) return (int)e;
     }
+    head_sums(st);   // (only if no fork took them)
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -2014,6 +2063,16 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     bytes += (size_t)round_up((int64_t)((net->n_prep > 0 ? net->n_prep : 1) * sizeof(ConvPrep)), 256);
     net->head_fusable = net->nodes.back().d.kind == LRS_NODE_CONV && net->nodes.back().d.bn == 0 &&
                         net->nodes.back().C <= 65535;
+    {
+        const auto &Lh = net->nodes.back();
+        net->head_pw = net->head_fusable && plain_unit(Lh.g) && Lh.wpre_off >= 0 && tune_knob("LRS_DIP_HEAD_PW", 1) != 0;
+        if (net->head_pw) {
+            net->hpart_off_bytes = (int64_t)bytes;   // [2][C][<= ceil(P / 64) workgroups]
+            bytes += (size_t)round_up(2 * (int64_t)Lh.C * ((Lh.P + 63) / 64) * 8, 256);
+            net->closs_off_bytes = (int64_t)bytes;
+            bytes += (size_t)round_up((int64_t)Lh.C * 8, 256);
+        }
+    }
     net->headcnt_off_bytes = (int64_t)bytes;   // C per-channel counters + the channel counter
     bytes += (size_t)round_up((int64_t)(net->nodes.back().C + 1) * 4, 256);
     net->misc_off_bytes = (int64_t)bytes;
@@ -2225,7 +2284,21 @@ static int ensure_side(lrs_dipnet *net, hipStream_t st) {
             return LRS_OK;
         }
     hipStream_t s = nullptr;
-    e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio);
+#ifdef LRS_TUNING
+    // A/B only: the side stream on a subset of the CUs (every k-th CU left to the critical stream)
+    static const int cuskip = (int)tune_knob("LRS_DIP_SIDE_CUSKIP", 0);
+    if (cuskip > 1) {
+        int dev = 0, ncu = 0;
+        if ((e = hipGetDevice(&dev)) == hipSuccess)
+            e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return (int)e;
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i)
+            if (i % cuskip != cuskip - 1) mask[(size_t)i / 32] |= 1u << (i % 32);
+        e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+    } else
+#endif
+        e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio);
     if (e != hipSuccess) return (int)e;
     net->sides.emplace_back(prio, s);
     net->side = s;

@@ -1,7 +1,7 @@
 """MPSNR trajectory of the ORACLE-driven LRS-PnP-DIP(1-Lip) outer loop on the bench's configs[2]
-cube (run in the BUILD CONTAINER only, ~5 min per seed on 8 cores):
+cube (run in the BUILD CONTAINER only, ~10 min per seed for 8 outer iterations on 6 cores):
 
-    OMP_NUM_THREADS=8 python tests/golden/gen_dip196_traj.py [seeds] [iters] [out.npz]   # -> dip196_traj_ref.npz
+    OMP_NUM_THREADS=6 python tests/golden/gen_dip196_traj.py 5 8 [out.npz]   # -> dip196_traj_ref.npz (5 seeds x 8)
 
 The reference's main_LRS_PnP_DIP_1-LiP.py cannot run this cube: its my_Lipschitz_Unet hardcodes
 128 bands (models/my_Lipschitz_Unet.py:33-101), and the cube has 198.  So the outer loop is the

@@ -68,8 +68,10 @@ def test_dip196_trajectory_vs_oracle_restatement(gpu, golden):
     iteration, early stopping off) against the oracle-driven restatement of the same outer loop
     (tests/golden/gen_dip196_traj.py: the C ISTA, oracle/dip_ref.py's torch U-Net with full-SVD
     sigma_max and torch Adam, the C X / dual update; the reference main itself cannot run 198 bands).
-    Per outer iteration, the mean MPSNR over the GPU's seeds equals the restatement's mean over its
-    seeds within three standard errors of the difference + 0.01 dB (the rule of the 36 x 36 test)."""
+    Per outer iteration (8 of them since round 6: the bench's MPSNR keeps falling past the first, so the
+    pin covers the stretch where it does), the mean MPSNR over the GPU's seeds equals the restatement's
+    mean over its seeds within three standard errors of the difference + 0.01 dB (the rule of the
+    36 x 36 test)."""
     from lrspnp import LrsPnP, LrsPnPConfig
     from lrspnp.data import load_fixture, mask_matrix, synthetic_cube, synthetic_dictionary, unfold
     from lrspnp.dip import DipConfig
