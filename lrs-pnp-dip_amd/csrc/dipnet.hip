@@ -1767,7 +1767,10 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
                 // main stream's scratch, free by then, beside whatever the side stream still runs
                 if (net->fork_w && (rc = flush_w(i))) return rc;
                 int wsplit = 1;
-                const bool defer = pw && t == 0 && i == first_conv;
+                // (LRS_DIP_DEFER_EXPLICIT=0, tuning only: the explicit (small-map) input conv's sum by
+                // k_gemm_reduce instead, as before round 6)
+                static const bool defer_explicit = tune_knob("LRS_DIP_DEFER_EXPLICIT", 1) != 0;
+                const bool defer = pw && t == 0 && i == first_conv && (defer_explicit || N.col_off < 0);
                 if ((rc = weight_grad(net, i, x, st, net->f(net->part_off), defer ? &wsplit : nullptr))) return rc;
                 if (defer && wsplit > 1)
                     *pw = AdamPend{net->f(net->part_off), wsplit, N.w_off, (int64_t)N.C * N.Kc,
@@ -2065,7 +2068,11 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
                         net->nodes.back().C <= 65535;
     {
         const auto &Lh = net->nodes.back();
-        net->head_pw = net->head_fusable && plain_unit(Lh.g) && Lh.wpre_off >= 0 && tune_knob("LRS_DIP_HEAD_PW", 1) != 0;
+        // only on small maps: 36^2 step 0.578 -> 0.571 ms, but 196^2 1.187 -> 1.192 ms (3 interleaved rounds,
+        // profiles/r06/ab/fused_head.txt): there the epilogue's extra 60 MB (target in, gz out) lengthens
+        // the 481-workgroup conv by more than the separate k_mse_head launch costs
+        net->head_pw = net->head_fusable && plain_unit(Lh.g) && Lh.wpre_off >= 0 && tune_knob("LRS_DIP_HEAD_PW", 1) != 0 &&
+                       Lh.P <= tune_knob("LRS_DIP_HEAD_PW_MAXP", 4096);
         if (net->head_pw) {
             net->hpart_off_bytes = (int64_t)bytes;   // [2][C][<= ceil(P / 64) workgroups]
             bytes += (size_t)round_up(2 * (int64_t)Lh.C * ((Lh.P + 63) / 64) * 8, 256);
