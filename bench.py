@@ -28,7 +28,7 @@ Rank 0 prints one JSON line with
   roofline     : the dominant stage — the DIP training of one outer iteration (dip workloads) or
                  the ISTA kernel (pnp): algorithmic MFMA FLOPs / time from HIP events on the stream
                  it runs on, vs the 157.3 TFLOP/s f32 MFMA peak; `traffic` = HBM bytes from the
-                 committed rocprofv3 PMC pass (profiles/r05/traffic.json), per the same unit;
+                 committed rocprofv3 PMC pass (profiles/r06/traffic.json), per the same unit;
                  `peak_split_bf16` / `frac_split_bf16`: the same work against the split-bf16
                  matrix-core ceiling (6 bf16 MFMAs per fp32-accurate product).
                  `roofline.kernels` adds the sparse-coding kernel (k_ista_rs / k_ista_ln2) per launch.
@@ -59,7 +59,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md chip table (f32 MFMA = f
 # per clock per SIMD x 4 x 256 CUs x 2.4 GHz = 2,517 TFLOP/s of bf16, / 6 = the ceiling of fp32-accurate
 # work on the bf16 matrix cores.
 SPLIT_BF16_PEAK_TFLOPS = 2516.6 / 6
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r05", "traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r06", "traffic.json")
 
 
 def parse():
@@ -140,7 +140,7 @@ def make_problem(H, W, B, bb, K, seed, mask="tiled", data="synthetic"):
 
 
 def load_traffic(key, profiled=True):
-    """HBM bytes of the committed PMC pass (profiles/r05/traffic.json); None for a configuration
+    """HBM bytes of the committed PMC pass (profiles/r06/traffic.json); None for a configuration
     other than the profiled default one."""
     if not profiled:
         return None

@@ -115,7 +115,9 @@ Split choose_split(int M, int N, int K, int precision = LRS_DIP_SPLIT_BF16, bool
     const bool big = force_big || t128 >= 64 || (precision == LRS_DIP_SPLIT_BF16 && K >= 8192 && t128 >= 4) || deep;
     const int64_t tiles = big ? t128 : (int64_t)((M + kBM64 - 1) / kBM64) * ((N + kBN64 - 1) / kBN64);
     int S = 1;
-    if (tiles < 256) {
+    // split-K below this many tiles (LRS_DIP_SPLIT_MIN_TILES, tuning only)
+    static const int64_t min_tiles = tune_knob("LRS_DIP_SPLIT_MIN_TILES", 256);
+    if (tiles < min_tiles) {
         S = (int)((target + tiles - 1) / tiles);   // ~2 workgroups per CU (256 and 1024 measured slower)
         const int smax = deep ? K / 512 : (K + 127) / 128;
         if (S > smax) S = smax;
