@@ -1240,6 +1240,13 @@ struct lrs_dipnet {
     bool sn_overlap = false;
     int n_prep_side = 0;
     int64_t prep_head_off_bytes = 0, prep_side_off_bytes = 0;
+    // prep_split: the data-gradient planes (read first in the backward) prepared on the side stream beside
+    // the forward; the forward planes and W / scale stay where they were (prep_f: forward / prep_fs: the
+    // overlapped side table, without the data-gradient planes; prep_d: the data-gradient planes only)
+    bool prep_split = false, wd_pending = false;
+    int n_prep_d = 0;
+    int64_t prep_f_off_bytes = 0, prep_fs_off_bytes = 0, prep_d_off_bytes = 0;
+    hipEvent_t ev_wdgo = nullptr, ev_wd = nullptr;
     hipEvent_t ev_head = nullptr, ev_sigma = nullptr;
     // split_ev: ev_sigma right after the Lanczos (the first BatchNorm needs the scale only) and ev_prep
     // after the other convs' planes (the second conv waits for it); else ev_sigma after both
@@ -1286,6 +1293,9 @@ struct lrs_dipnet {
     ConvPrep *prep() const { return (ConvPrep *)(ws + prep_off_bytes); }
     ConvPrep *prep_head() const { return (ConvPrep *)(ws + prep_head_off_bytes); }
     ConvPrep *prep_side() const { return (ConvPrep *)(ws + prep_side_off_bytes); }
+    ConvPrep *prep_f() const { return (ConvPrep *)(ws + prep_f_off_bytes); }
+    ConvPrep *prep_fs() const { return (ConvPrep *)(ws + prep_fs_off_bytes); }
+    ConvPrep *prep_d() const { return (ConvPrep *)(ws + prep_d_off_bytes); }
     int *headcnt() const { return (int *)(ws + headcnt_off_bytes); }
     double *loss_acc() const { return (double *)(ws + misc_off_bytes); }
     int *step() const { return (int *)(ws + misc_off_bytes + 8); }
@@ -1337,8 +1347,18 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
         if (rc) return rc;
     }
     if (net->n_prep && !raw_first) {   // W / scale and the bf16 planes of every conv, one launch
-        hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep), dim3(256), 0, st, net->prep(), net->f(net->scale_off),
-                           step_begin ? net->loss_acc() : nullptr, net->step());
+        const bool split = net->prep_split && step_begin && net->side && net->ev_wdgo && net->ev_wd;
+        hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep), dim3(256), 0, st, split ? net->prep_f() : net->prep(),
+                           net->f(net->scale_off), step_begin ? net->loss_acc() : nullptr, net->step());
+        if (split && net->n_prep_d) {   // the data-gradient planes beside the forward (the backward waits)
+            hipError_t e = hipEventRecord(net->ev_wdgo, st);
+            if (e == hipSuccess) e = hipStreamWaitEvent(net->side, net->ev_wdgo, 0);
+            if (e != hipSuccess) return (int)e;
+            hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep_d), dim3(256), 0, net->side, net->prep_d(),
+                               net->f(net->scale_off), (double *)nullptr, net->step());
+            if ((e = hipEventRecord(net->ev_wd, net->side)) != hipSuccess) return (int)e;
+            net->wd_pending = true;
+        }
         LRS_CHECK_LAUNCH();
     }
     bool prep_waited = !(raw_first && net->split_ev);
@@ -1460,8 +1480,15 @@ int dipnet_forward(lrs_dipnet *net, const float *x, hipStream_t st, bool step_be
     return LRS_OK;
 }
 
+struct EsJob {   // the early-stopping update of this step's output, run beside the backward (dipnet_step)
+    const float *out;
+    int64_t N;
+    float *ring;
+    lrs_es_state *es;
+};
+int es_update(const float *out, int64_t N, float *ring, lrs_es_state *es, hipStream_t st);
 int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done = false, AdamPend *pw = nullptr,
-                    bool head_reduce = false);
+                    bool head_reduce = false, const EsJob *esj = nullptr);
 int mse_head(lrs_dipnet *net, const float *out, const float *target, const float *mask, hipStream_t st);
 
 // k_mse_head over the last node (conv without BN): gz and the bias gradient of that node, + loss
@@ -1509,11 +1536,19 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
         hipLaunchKernelGGL(k_sn_sigma, dim3(net->n_sn), dim3(256), 0, net->side, net->table(), net->gram(),
                            net->f(net->sigma_off), net->f(net->scale_off), net->ln_lambda, (long long *)nullptr);
         if (net->split_ev && (e = hipEventRecord(net->ev_sigma, net->side)) != hipSuccess) return (int)e;
+        const bool split = net->prep_split && net->ev_wd;
         if (net->n_prep_side)
             hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep_side), dim3(256), 0, net->side,
-                               net->prep_side(), net->f(net->scale_off), (double *)nullptr, net->step());
+                               split ? net->prep_fs() : net->prep_side(), net->f(net->scale_off), (double *)nullptr,
+                               net->step());
         e = hipEventRecord(net->split_ev ? net->ev_prep : net->ev_sigma, net->side);
         if (e != hipSuccess) return (int)e;
+        if (split && net->n_prep_d) {   // the data-gradient planes after the forward's (the backward waits)
+            hipLaunchKernelGGL(k_conv_prep, dim3(prep_blocks(), net->n_prep_d), dim3(256), 0, net->side, net->prep_d(),
+                               net->f(net->scale_off), (double *)nullptr, net->step());
+            if ((e = hipEventRecord(net->ev_wd, net->side)) != hipSuccess) return (int)e;
+            net->wd_pending = true;
+        }
         LRS_CHECK_LAUNCH();
     }
     const int n = (int)net->nodes.size();
@@ -1538,12 +1573,16 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
     // the input conv's weight-gradient split-K sum is finished inside Adam (one launch less on the
     // step's tail)
     AdamPend pw{};
-    rc = dipnet_backward(net, x, st, net->head_fusable, &pw, fused_head);
+    // (LRS_DIP_ES_SIDE=0, tuning only: the ES update after Adam on this stream, as until round 6)
+    static const bool es_side = tune_knob("LRS_DIP_ES_SIDE", 1) != 0;
+    const EsJob esj{out, (int64_t)Lst.C * Lst.P, ring, es};
+    const bool es_beside = es && es_side && net->fork_w;
+    rc = dipnet_backward(net, x, st, net->head_fusable, &pw, fused_head, es_beside ? &esj : nullptr);
     if (rc) return rc;
     hipLaunchKernelGGL(k_adam, dim3(ew_blocks((net->n_params + 3) / 4, 8192)), dim3(kEw), 0, st, net->params,
                        (const float *)net->grads, net->am, net->av, net->n_params, (const int *)net->step(), lr, b1, b2,
                        eps, pw);
-    if (es) {
+    if (es && !es_beside) {
         rc = es_update(out, (int64_t)Lst.C * Lst.P, ring, es, st);
         if (rc) return rc;
     }
@@ -1678,9 +1717,18 @@ int group_bwd_conv(lrs_dipnet *net, int i, const float *x, float *gx, int accum_
 
 // pw (lrs_dipnet_train_steps): the input conv's weight gradient may leave its split-K partials for
 // k_adam to finish (AdamPend; pw->part == nullptr when nothing is pending)
-int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done, AdamPend *pw, bool head_reduce) {
+int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_done, AdamPend *pw, bool head_reduce,
+                    const EsJob *esj) {
     int rc;
     const int n = (int)net->nodes.size();
+    // the ES update reads only the forward's output and its own ring: on the side stream with the first
+    // weight gradients (its ring slot and window sums follow the previous step's there), joined before Adam
+    auto es_side = [&](hipStream_t hs) -> int {
+        if (!esj) return LRS_OK;
+        const int r = es_update(esj->out, esj->N, esj->ring, esj->es, hs);
+        esj = nullptr;
+        return r;
+    };
     // the fused loss head's sums (PwHead): the bias gradient of the last conv (read by Adam only) and the
     // loss, on the side stream with the first weight gradients (or here, without a side stream)
     auto head_sums = [&](hipStream_t hs) {
@@ -1692,6 +1740,11 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
         head_reduce = false;
     };
     if (!net->fork_w) head_sums(st);
+    if (net->wd_pending) {   // the data-gradient planes prepared on the side stream (prep_split)
+        const hipError_t e = hipStreamWaitEvent(st, net->ev_wd, 0);
+        if (e != hipSuccess) return (int)e;
+        net->wd_pending = false;
+    }
     // gradient buffers: the first contribution to a tensor writes, later ones accumulate
     std::vector<char> written(n + 1, 0);
     written[n] = 1;
@@ -1706,6 +1759,7 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
         if (e == hipSuccess) e = hipStreamWaitEvent(net->side, net->ev_fork[j], 0);
         if (e != hipSuccess) return (int)e;
         head_sums(net->side);
+        if (const int r = es_side(net->side)) return r;
         for (int q : wq)
             if (const int r = weight_grad(net, q, x, net->side, net->f(net->part2_off))) return r;
         wq.clear();
@@ -1859,6 +1913,7 @@ int dipnet_backward(lrs_dipnet *net, const float *x, hipStream_t st, bool head_d
         if (e != hipSuccess) return (int)e;
     }
     head_sums(st);   // (only if no fork took them)
+    if ((rc = es_side(st))) return rc;
     LRS_CHECK_LAUNCH();
     return LRS_OK;
 }
@@ -2066,6 +2121,19 @@ extern "C" int lrs_dipnet_create(const lrs_dip_node *nodes, int n_nodes, int C, 
     bytes += 256;   // one ConvPrep
     net->prep_side_off_bytes = (int64_t)bytes;
     bytes += (size_t)round_up((int64_t)((net->n_prep > 0 ? net->n_prep : 1) * sizeof(ConvPrep)), 256);
+    {
+        const int64_t tb = round_up((int64_t)((net->n_prep > 0 ? net->n_prep : 1) * sizeof(ConvPrep)), 256);
+        net->prep_f_off_bytes = (int64_t)bytes;
+        bytes += (size_t)tb;
+        net->prep_fs_off_bytes = (int64_t)bytes;
+        bytes += (size_t)tb;
+        net->prep_d_off_bytes = (int64_t)bytes;
+        bytes += (size_t)tb;
+        // off: 196^2 1.189 -> 1.192 ms, 36^2 0.572 -> 0.576 ms with it (3 interleaved rounds,
+        // profiles/r06/ab/prep_split_dropped.txt): the extra event and launch cost more than the half of
+        // the preparation it takes off the critical stream (LRS_DIP_PREP_SPLIT=1, tuning only)
+        net->prep_split = net->fork_w && net->n_prep > 0 && tune_knob("LRS_DIP_PREP_SPLIT", 0) != 0;
+    }
     net->head_fusable = net->nodes.back().d.kind == LRS_NODE_CONV && net->nodes.back().d.bn == 0 &&
                         net->nodes.back().C <= 65535;
     {
@@ -2102,6 +2170,8 @@ extern "C" void lrs_dipnet_destroy(lrs_dipnet *net) {
     if (net->ev_head) (void)hipEventDestroy(net->ev_head);
     if (net->ev_sigma) (void)hipEventDestroy(net->ev_sigma);
     if (net->ev_prep) (void)hipEventDestroy(net->ev_prep);
+    if (net->ev_wdgo) (void)hipEventDestroy(net->ev_wdgo);
+    if (net->ev_wd) (void)hipEventDestroy(net->ev_wd);
     for (auto &ps : net->sides) (void)hipStreamDestroy(ps.second);
     delete net;
 }
@@ -2184,6 +2254,26 @@ extern "C" int lrs_dipnet_bind(lrs_dipnet *net, float *params, float *grads, flo
         if (e == hipSuccess) e = hipMemcpy(net->prep_head(), &head, sizeof(ConvPrep), hipMemcpyHostToDevice);
         if (e == hipSuccess)
             e = hipMemcpy(net->prep_side(), side.data(), sizeof(ConvPrep) * side.size(), hipMemcpyHostToDevice);
+    }
+    if (net->prep_split && !prep.empty()) {
+        std::vector<ConvPrep> pf(prep), pd;
+        for (auto &c : pf) c.wd = nullptr;
+        for (const auto &c : prep)
+            if (c.wd) {
+                ConvPrep d = c;
+                d.Wn = nullptr;
+                d.wf = nullptr;
+                pd.push_back(d);
+            }
+        net->n_prep_d = (int)pd.size();
+        if (e == hipSuccess) e = hipMemcpy(net->prep_f(), pf.data(), sizeof(ConvPrep) * pf.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess && !pd.empty())
+            e = hipMemcpy(net->prep_d(), pd.data(), sizeof(ConvPrep) * pd.size(), hipMemcpyHostToDevice);
+        if (net->sn_overlap) {
+            std::vector<ConvPrep> fs(pf);
+            fs[0].wf = nullptr;   // (the first conv's forward planes: the head slot, raw weights)
+            if (e == hipSuccess) e = hipMemcpy(net->prep_fs(), fs.data(), sizeof(ConvPrep) * fs.size(), hipMemcpyHostToDevice);
+        }
     }
     if (e == hipSuccess) e = hipMemset(net->misc_off_bytes + net->ws, 0, 256);
     if (e == hipSuccess) e = hipMemset(net->headcnt(), 0, sizeof(int) * (net->nodes.back().C + 1));
@@ -2321,6 +2411,8 @@ static int ensure_side(lrs_dipnet *net, hipStream_t st) {
     if (e == hipSuccess && !net->ev_head) e = hipEventCreateWithFlags(&net->ev_head, evf);
     if (e == hipSuccess && !net->ev_sigma) e = hipEventCreateWithFlags(&net->ev_sigma, evf);
     if (e == hipSuccess && !net->ev_prep) e = hipEventCreateWithFlags(&net->ev_prep, evf);
+    if (e == hipSuccess && !net->ev_wdgo) e = hipEventCreateWithFlags(&net->ev_wdgo, evf);
+    if (e == hipSuccess && !net->ev_wd) e = hipEventCreateWithFlags(&net->ev_wd, evf);
     for (size_t i = 0; i < net->ev_fork.size() && e == hipSuccess; ++i)
         if (!net->ev_fork[i]) e = hipEventCreateWithFlags(&net->ev_fork[i], evf);
     return (int)e;
