@@ -140,3 +140,13 @@ def test_workspace_sized_from_n_pad():
                           None) == -3
     # sized from n_pad instead, the same calls pass the check (then need a device: not called here)
     assert L.lrs_ista_pat_workspace(n_pad, K, npat) > ws and L.lrs_ista_workspace(n_pad, K, 0, None) > wr
+
+
+def test_es_ring_bytes():
+    """lrs_es_ring_bytes: the ring [size][N] floats (16-B aligned), then the fp64 window sums A, B [N] and
+    the workgroup partials (kEsMaxBlocks doubles); 0 for a bad size."""
+    L = _lib.lib()
+    for size, N in [(30, 128 * 36 * 36), (30, 198 * 196 * 196), (7, 13)]:
+        ring = (size * N * 4 + 15) // 16 * 16
+        assert L.lrs_es_ring_bytes(size, N) == ring + 2 * N * 8 + 1024 * 8
+    assert L.lrs_es_ring_bytes(0, 10) == 0 and L.lrs_es_ring_bytes(30, 0) == 0

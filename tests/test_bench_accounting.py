@@ -38,3 +38,22 @@ def test_unet_196_is_one_gigabyte_per_step():
     net = NS(nodes=nodes, in_shape=(198, 196, 196), shapes=[(c, h, h) for c, h in dims], n_params=434000)
     b = bench.dip_alg_bytes_per_step(net)
     assert 0.95e9 < b < 1.05e9, b
+
+
+def test_cpu_baseline_host_fields():
+    """The CPU baseline records the cores it used beside nproc, the machine's CPUs, the affinity set, the
+    cgroup quota and the CPU model; by default it uses every CPU it may run on."""
+    saved = os.environ.pop("OMP_NUM_THREADS", None)
+    try:
+        t = bench._threads()
+        machine, aff, quota, model = bench.host_cpus()
+        assert t == max(1, min(aff, int(quota)) if quota else aff)
+        f = bench.host_fields(t)
+        for k in ("cores", "nproc", "machine_cpus", "affinity_cpus", "cgroup_cpu_quota", "cpu_model"):
+            assert k in f, k
+        assert f["cores"] == t and f["machine_cpus"] == machine
+    finally:
+        if saved is None:
+            os.environ.pop("OMP_NUM_THREADS", None)
+        else:
+            os.environ["OMP_NUM_THREADS"] = saved
