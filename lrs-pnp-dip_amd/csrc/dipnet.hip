@@ -152,9 +152,9 @@ int64_t gemm_part_floats(int M, int N, int K) {
 // conv's ConvGeom::prec
 int gemm(int prec, int TA, int TB, const float *A, const float *B, float *C, const float *bias, const float *div, int M,
          int N, int K, float *part, int64_t part_cap, hipStream_t st, int accum = 0, int *nsplit_out = nullptr,
-         bool force_big = false) {
+         bool force_big = false, int target = 512) {
     if (M <= 0 || N <= 0) return LRS_OK;
-    const Split s = choose_split(M, N, K, prec, force_big);
+    const Split s = choose_split(M, N, K, prec, force_big, target);
     if (nsplit_out) *nsplit_out = s.S;   // > 1: the caller finishes the split-K sum (no reduce here)
     GemmArgs g{A, B, C, bias, div, M, N, K, s.kchunk, accum};
     if (s.S > 1) {
@@ -476,9 +476,9 @@ int upc_dgrad(const ConvGeom &g, const float *gz, const __bf16 *wd, int Cout, fl
 // split-K over gridDim.z, partials [split][cls][Cout][4 Cin] in part), then k_upc_wgrad_combine sums
 // splits and classes into dW (/ *div).
 int upc_wgrad(const ConvGeom &g, const float *gz, const float *x, const float *div, int Cout, float *gw, float *part,
-              int64_t part_cap, hipStream_t st) {
+              int64_t part_cap, hipStream_t st, int target = 512) {
     const int Q = g.Hs * g.Ws, N = 4 * g.Cin;
-    const Split s = choose_split(Cout, 4 * N, Q, LRS_DIP_SPLIT_BF16, true);
+    const Split s = choose_split(Cout, 4 * N, Q, LRS_DIP_SPLIT_BF16, true, target);
     if (!part || part_cap < (int64_t)s.S * 4 * Cout * N) return LRS_E_WORKSPACE;
     const GemmArgs a{nullptr, nullptr, part, nullptr, nullptr, Cout, N, Q, s.kchunk, 0, 4, g.Ws, 0, 0};
     const dim3 grid((N + 127) / 128, (Cout + 127) / 128, 4 * s.S);
@@ -626,7 +626,7 @@ int conv_fwd(const ConvGeom &g, const float *x, const float *w, const float *bia
 // weight planes (wprep) for the stride-1 data gradient.
 int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *w, const float *div, int Cout,
              float *gx, float *gw, float *dcol, float *part, int64_t part_cap, hipStream_t st, int accum_gx = 0,
-             bool implicit = false, const __bf16 *wpre = nullptr, int *wsplit_out = nullptr) {
+             bool implicit = false, const __bf16 *wpre = nullptr, int *wsplit_out = nullptr, int wtarget = 512) {
     const int P = g.Ho * g.Wo, kk = g.k * g.k, Kc = g.Cin * kk;
     int rc;
     implicit = implicit && !plain_unit(g);
@@ -637,14 +637,15 @@ int conv_bwd(const ConvGeom &g, const float *gz, const float *col, const float *
         if (!conv_implicit_ok(g, Cout)) return LRS_E_UNSUPPORTED;
         // wsplit_out: the caller finishes the split-K sum (k_adam's AdamPend)
         rc = gemm_s3_conv(LdDense<true>{gz, P, Cout}, LdWgradTM{col, g.Cin * g.Hs * g.Ws * 4, g, nullptr, 0}, gw,
-                          nullptr, div, Cout, Kc, P, part, part_cap, st, wsplit_out);
+                          nullptr, div, Cout, Kc, P, part, part_cap, st, wsplit_out, 0, wtarget);
     } else {
         // a 1x1 conv's weight gradient (K = all pixels): 128-tiles with deep split-K on the split-bf16
         // kernel (A/B in the 196^2 training step, configs[2]: 5.50 -> 5.65 outer it/s against the f32
         // 64-tile kernel; alone the two are within 12 %, but the f32 kernel's 512 workgroups hold the
         // CUs the concurrent data-gradient chain needs for longer)
         // (wsplit_out: as above, the caller's k_adam finishes the split-K sum)
-        rc = gemm(g.prec, 0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st, 0, wsplit_out, plain_unit(g));
+        rc = gemm(g.prec, 0, 1, gz, col, gw, nullptr, div, Cout, Kc, P, part, part_cap, st, 0, wsplit_out, plain_unit(g),
+                  wtarget);
     }
     if (rc || !gx) return rc;
     if (plain_unit(g) && wpre)      // 1x1 data gradient: W^T planes (wprep's WD)
@@ -816,12 +817,13 @@ int bn_bwd(const float *gy, const float *y, const float *z, const float *gamma, 
 __global__ __launch_bounds__(256) void k_sn_gram_head(const SnConv *convs, double *gram, int n, const ConvPrep *head,
                                                      double *loss_acc, int *step) {
     __shared__ float Ws[128][36];
-    if ((int)blockIdx.y == n) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) {   // a training step begins
+    if ((int)blockIdx.y >= n) {   // rows n, n + 1, ...: the planes
+        const int64_t b = (int64_t)(blockIdx.y - n) * gridDim.x + blockIdx.x;
+        if (b == 0 && threadIdx.x == 0) {   // a training step begins
             *loss_acc = 0.0;
             *step += 1;
         }
-        conv_prep_body(*head, 1.0f, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+        conv_prep_body(*head, 1.0f, b * blockDim.x + threadIdx.x, (int64_t)(gridDim.y - n) * gridDim.x * blockDim.x);
         return;
     }
     const SnConv cv = convs[blockIdx.y];
@@ -1527,7 +1529,11 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
         // conv but the first on the side stream beside the first conv, whose planes come from the raw
         // weights here
         // (the Gram reduce too: on the side stream beside the first conv it took 23 us instead of 6)
-        hipLaunchKernelGGL(k_sn_gram_head, dim3(kSnSplit, net->n_sn + 1), dim3(256), 0, st, net->table(), net->gram(),
+        // the first conv's planes on 8 grid rows of kSnSplit workgroups (one row: the kernel took 36.7 us,
+        // its 16 plane workgroups the longest; 8 rows: 19.2 us, 196^2 step 1.194 -> 1.177 ms, 3 interleaved
+        // rounds, profiles/r06/ab/head_plane_rows.txt; LRS_DIP_HEAD_PLANE_ROWS, tuning only)
+        static const int prow = (int)std::max<int64_t>(1, std::min<int64_t>(64, tune_knob("LRS_DIP_HEAD_PLANE_ROWS", 8)));
+        hipLaunchKernelGGL(k_sn_gram_head, dim3(kSnSplit, net->n_sn + prow), dim3(256), 0, st, net->table(), net->gram(),
                            net->n_sn, (const ConvPrep *)net->prep_head(), net->loss_acc(), net->step());
         hipLaunchKernelGGL(k_sn_gram_reduce, dim3(kSnPairs, net->n_sn), dim3(256), 0, st, net->table(), net->gram());
         hipError_t e = hipEventRecord(net->ev_head, st);
@@ -1594,8 +1600,16 @@ int dipnet_step(lrs_dipnet *net, const float *x, const float *target, const floa
 // gradient into net->grads (the input gets none: the reference's DIP input needs no gradient).
 // Weight gradient of conv node i on stream ws: reads dL/dz, the layer input and the scale only.
 // scratch: its split-K partials (part2 on the side stream; part on the main one)
+// split-K workgroup target of the weight gradients on the side stream (LRS_DIP_WGRAD_SPLIT_WG, tuning
+// only): fewer splits write fewer partials and hold fewer CUs beside the data-gradient chain
+inline int wgrad_split_target() {
+    static const int v = (int)std::max<int64_t>(1, std::min<int64_t>(512, tune_knob("LRS_DIP_WGRAD_SPLIT_WG", 512)));
+    return v;
+}
+
 int weight_grad(lrs_dipnet *net, int i, const float *x, hipStream_t ws, float *scratch, int *wsplit_out = nullptr) {
     if (wsplit_out) *wsplit_out = 1;
+    const int wt = ws == net->side ? wgrad_split_target() : 512;
     auto &N = net->nodes[i];
     const int t = N.d.in0;
     const float *gz = net->f(N.gz_off);
@@ -1617,9 +1631,9 @@ int weight_grad(lrs_dipnet *net, int i, const float *x, hipStream_t ws, float *s
         hipLaunchKernelGGL(k_im2col, grid, dim3(256), 0, ws, net->tensor(t, x), N.g, net->f(N.col_off));
     }
     if (N.upc)
-        return upc_wgrad(N.g, gz, net->tensor(t, x), wdiv, N.C, net->grads + N.w_off, scratch, net->part_cap, ws);
+        return upc_wgrad(N.g, gz, net->tensor(t, x), wdiv, N.C, net->grads + N.w_off, scratch, net->part_cap, ws, wt);
     return conv_bwd(N.g, gz, colsrc, w, wdiv, N.C, nullptr, net->grads + N.w_off, nullptr, scratch, net->part_cap, ws, 0,
-                    N.col_off < 0, nullptr, wsplit_out);
+                    N.col_off < 0, nullptr, wsplit_out, wt);
 }
 
 // Is conv node i a fork point of the weight-gradient side stream (Node::fork_pt, lrs_dipnet_create)?
