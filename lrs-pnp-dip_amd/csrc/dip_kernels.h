@@ -538,11 +538,13 @@ __global__ __launch_bounds__(256) void k_col2im(const float *__restrict__ dcol, 
 // Wave / block reductions.  Doubles go through DPP row operations (no LDS crossbar): after four
 // steps every 16-lane row holds its row sum, then readlane gathers the four rows.
 // ------------------------------------------------------------------------------------------
+// (full-row permutations only: every lane reads a lane of its own row, so no 'old' value is needed
+// -- mov_dpp instead of update_dpp(0, ...) saves the zeroing of each destination)
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
@@ -1522,10 +1524,10 @@ __device__ __forceinline__ double sn_grid(double base, double step, int t) { ret
 
 // max over the 64 lanes (uniform): DPP row steps, then the four rows' values by readlane
 __device__ __forceinline__ int wave_max_i(int v) {
-    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
-    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
-    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
-    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));   // row_mirror
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true));   // row_half_mirror
+    v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true));   // row_mirror
     return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
                max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
@@ -1653,8 +1655,9 @@ __global__ __launch_bounds__(256) void k_sn_sigma(const SnConv *convs, const dou
             u4[i] += dpp_d<0x4E>(u4[i]);
             u4[i] += dpp_d<0x141>(u4[i]);
         }
-        const int own = cb & 3;
-        double u = own == 0 ? u4[0] : own == 1 ? u4[1] : own == 2 ? u4[2] : u4[3];
+        const int own = cb & 3;   // (selects, not a branch per lane group)
+        const double u01 = (own & 1) ? u4[1] : u4[0], u23 = (own & 1) ? u4[3] : u4[2];
+        double u = (own & 2) ? u23 : u01;
         const double w_rr = wave_sum_d(half == 0 ? rr * rr : 0.0);
         const double w_ru = wave_sum_d(half == 0 ? rr * u : 0.0);
         if ((t & 63) == 0) {
