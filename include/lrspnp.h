@@ -328,7 +328,8 @@ int lrs_image_to_unfolded_f32(const float *img, int64_t H, int64_t W, int64_t B,
 /* Early stopping state (device memory).  lrs_es_init fills it; every lrs_es_update_f32 pushes one
  * output into the ring and, once full, applies the variance test.  ring: lrs_es_ring_bytes(size, N)
  * bytes of device memory -- the last `size` outputs as [size][N] floats (slot = epoch % size), then
- * the per-pixel window sums the test slides from step to step. */
+ * the per-pixel window sums (fp64) and the window's sum of squares that the test slides from step to
+ * step. */
 typedef struct {
     int32_t count, size, patience, wait, stop, stop_epoch, best_epoch, reserved;
     double best, var_acc, last_var;

@@ -2012,17 +2012,24 @@ __global__ void k_step_begin(double *loss_acc, int *step) {
 // ------------------------------------------------------------------------------------------
 // Early stopping (main_LRS_PnP_DIP_1-LiP.py:71-99, 244-264), on device.
 // The reference's metric each step, once the last `size` outputs are collected (myMetric, :102-103):
-//   var = mean_j sum_p (ave_p - img_j,p)^2 / N = sum_p (B_p - A_p^2 / size) / (N size),
-// A_p = sum_j img_j,p and B_p = sum_j img_j,p^2 over the ring.  The buffer (lrs_es_ring_bytes) holds the
-// ring [size][N] floats, then A [N] and B [N] (fp64) and the per-workgroup partial sums.  One pass per
-// step (k_es_step) writes the new output into its slot and slides A and B (+ new - the slot's old
-// value: the squares are exact in fp64), so a step reads the ring slot it overwrites and nothing else;
-// every `size` steps (the slot of the last index) A and B are re-summed from the whole ring in slot
-// order, which bounds the sliding sums' rounding drift to `size` updates.  The per-workgroup partials
-// are summed in a fixed order by k_es_decide (deterministic; the round-5 form re-read the whole ring
-// twice per step -- 1.8 GB per step at 196 x 196 x 198 -- and added workgroup sums with atomics).
+//   var = mean_j sum_p (ave_p - img_j,p)^2 / N = (Q2 - sum_p A_p^2 / size) / (N size),
+// A_p = sum_j img_j,p over the ring and Q2 = sum_p sum_j img_j,p^2, one scalar (the squares' sum needs
+// no per-pixel form).  The buffer (lrs_es_ring_bytes) holds the ring [size][N] floats, then A [N]
+// (fp64), the per-workgroup partial sums [2][kEsMaxBlocks] and Q2.  One pass per step (k_es_step)
+// writes the new output into its slot and slides A (+ new - the slot's old value), so a step reads the
+// ring slot it overwrites and nothing else, and its workgroups sum the change of the squares (exact in
+// fp64: new^2 - old^2) and A_p^2; k_es_decide adds both in a fixed order (deterministic), slides Q2
+// and forms the variance.  Every kEsRefresh windows (the slot of the last index) A and Q2 are
+// re-summed from the whole ring in slot order, bounding the sliding sums' rounding drift (~1e-16 per
+// update: after 300 updates still ~1e-12 of the variance).  Traffic 28 B per output element per step
+// (round 6 first form: 44 B with a per-pixel B_p and a re-sum every window; round 5: the whole ring read
+// twice per step -- 1.8 GB per step at 196 x 196 x 198 -- and workgroup sums added with atomics).
 // ------------------------------------------------------------------------------------------
 constexpr int kEsMaxBlocks = 1024;
+constexpr int kEsRefresh = 10;   // windows between re-sums of A and Q2 from the ring
+
+// this output's epoch c (before k_es_decide increments count) re-sums A and Q2 from the ring
+__host__ __device__ inline bool es_refresh(int c, int S) { return (c + 1) % (S * kEsRefresh) == 0; }
 
 __host__ __device__ inline int64_t es_ab_offset_bytes(int size, int64_t N) {   // A after the ring, 16-B aligned
     return ((int64_t)size * N * 4 + 15) / 16 * 16;
@@ -2030,43 +2037,46 @@ __host__ __device__ inline int64_t es_ab_offset_bytes(int size, int64_t N) {   /
 
 __global__ __launch_bounds__(256) void k_es_step(const float *__restrict__ out, int64_t N, float *__restrict__ ring,
                                                 lrs_es_state *st) {
-    __shared__ double red[8];
+    __shared__ double red[16];
     const int S = st->size, c = st->count, slot = c % S;   // c: this output's epoch (k_es_decide increments count)
     double *A = reinterpret_cast<double *>(reinterpret_cast<char *>(ring) + es_ab_offset_bytes(S, N));
-    double *B = A + N, *part = B + N;
+    double *part = A + N;   // [0 .. kEsMaxBlocks): the squares' change (or sum), then the A^2 sums
     float *dst = ring + (int64_t)slot * N;
-    const bool full = c + 1 >= S, refresh = full && slot == S - 1;
-    double s = 0.0;
+    const bool full = c + 1 >= S, refresh = es_refresh(c, S);
+    double dq = 0.0, qa = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
         const float x = out[i];
-        double a, b;
+        double a;
         if (refresh) {   // the ring in slot order, the new output in the last slot
             dst[i] = x;
             a = 0.0;
-            b = 0.0;
+            double q = 0.0;
             for (int j = 0; j < S - 1; ++j) {
                 const double v = (double)ring[(int64_t)j * N + i];
                 a += v;
-                b += v * v;
+                q += v * v;
             }
             a += (double)x;
-            b += (double)x * (double)x;
-        } else if (c < S) {   // filling: a plain running sum (at c = S - 1 the refresh above)
+            q += (double)x * (double)x;
+            dq += q;
+        } else if (c < S) {   // filling: a plain running sum
             dst[i] = x;
             a = c == 0 ? (double)x : A[i] + (double)x;
-            b = c == 0 ? (double)x * (double)x : B[i] + (double)x * (double)x;
+            dq += (double)x * (double)x;
         } else {              // sliding: the slot's old output leaves the window
             const float o = dst[i];
             dst[i] = x;
             a = A[i] + ((double)x - (double)o);
-            b = B[i] + ((double)x * (double)x - (double)o * (double)o);
+            dq += (double)x * (double)x - (double)o * (double)o;
         }
         A[i] = a;
-        B[i] = b;
-        if (full) s += b - a * a / (double)S;
+        if (full) qa += a * a;
     }
-    s = block_sum_d(s, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    block_sum2_d(dq, qa, red);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = dq;
+        part[kEsMaxBlocks + blockIdx.x] = qa;
+    }
 }
 
 #ifdef LRS_TUNING
@@ -2101,12 +2111,25 @@ __global__ void k_es_var_r5(const float *__restrict__ ring, int64_t N, lrs_es_st
 // (nblk == 0: the round-5 form's var_acc instead)
 __global__ void k_es_decide(const float *ring, int64_t N, int nblk, lrs_es_state *st) {
     const int S = st->size;
-    const double *part = reinterpret_cast<const double *>(reinterpret_cast<const char *>(ring) + es_ab_offset_bytes(S, N)) + 2 * N;
-    double v = 0.0;
-    for (int b = threadIdx.x; b < nblk; b += 64) v += part[b];
-    v = wave_sum_d(v);   // fixed order
+    double *part = reinterpret_cast<double *>(reinterpret_cast<char *>(const_cast<float *>(ring)) + es_ab_offset_bytes(S, N)) + N;
+    double *q2 = part + 2 * kEsMaxBlocks;   // the window's sum of squares
+    double dq = 0.0, qa = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += 64) {
+        dq += part[b];
+        qa += part[kEsMaxBlocks + b];
+    }
+    dq = wave_sum_d(dq);   // fixed order
+    qa = wave_sum_d(qa);
     if (threadIdx.x != 0) return;
-    if (nblk == 0) v = st->var_acc;
+    double v;
+    if (nblk == 0) {
+        v = st->var_acc;
+    } else {
+        const int c = st->count;
+        const double q = (c == 0 || es_refresh(c, S)) ? dq : *q2 + dq;
+        *q2 = q;
+        v = q - qa / (double)S;
+    }
     const int epoch = st->count;           // iteration index i of the reference loop
     st->count += 1;
     if (st->count >= S && !st->stop) {

@@ -1196,7 +1196,7 @@ extern "C" int lrs_es_init(lrs_es_state *st, int size, int patience, void *strea
 
 extern "C" size_t lrs_es_ring_bytes(int size, int64_t N) {
     if (size <= 0 || N <= 0) return 0;
-    return (size_t)(es_ab_offset_bytes(size, N) + 2 * N * 8 + kEsMaxBlocks * 8);
+    return (size_t)(es_ab_offset_bytes(size, N) + N * 8 + (2 * kEsMaxBlocks + 2) * 8);
 }
 
 extern "C" int lrs_es_update_f32(const float *out, int64_t N, float *ring, lrs_es_state *st, void *stream) {

@@ -143,10 +143,11 @@ def test_workspace_sized_from_n_pad():
 
 
 def test_es_ring_bytes():
-    """lrs_es_ring_bytes: the ring [size][N] floats (16-B aligned), then the fp64 window sums A, B [N] and
-    the workgroup partials (kEsMaxBlocks doubles); 0 for a bad size."""
+    """lrs_es_ring_bytes: the ring [size][N] floats (16-B aligned), then the fp64 window sums A [N], the
+    workgroup partials (2 x kEsMaxBlocks doubles) and the window's sum of squares (+ one spare double);
+    0 for a bad size."""
     L = _lib.lib()
     for size, N in [(30, 128 * 36 * 36), (30, 198 * 196 * 196), (7, 13)]:
         ring = (size * N * 4 + 15) // 16 * 16
-        assert L.lrs_es_ring_bytes(size, N) == ring + 2 * N * 8 + 1024 * 8
+        assert L.lrs_es_ring_bytes(size, N) == ring + N * 8 + (2 * 1024 + 2) * 8
     assert L.lrs_es_ring_bytes(0, 10) == 0 and L.lrs_es_ring_bytes(30, 0) == 0
