@@ -277,8 +277,10 @@ class DipNet:
         return buf[off:off + 4 * n].view(torch.float32).view(*self.out_shape)
 
     def train_steps(self, x, target, mask, nsteps: int, lr: float = 0.1, betas=(0.9, 0.999),
-                    eps: float = 1e-8, es=None, use_graph: bool = True):
-        """nsteps of: forward, masked MSE, backward, Adam (and the ES update when es is given)."""
+                    eps: float = 1e-8, es=None, use_graph: bool = False):
+        """nsteps of: forward, masked MSE, backward, Adam (and the ES update when es is given).
+        use_graph: replay one captured hipGraph per step instead of the eager launches (bit-identical,
+        measured slower: DESIGN.md §5 -- off by default, as in DipConfig)."""
         import torch
         self.stream.wait_stream(torch.cuda.current_stream())
         rc = self.L.lrs_dipnet_train_steps(
