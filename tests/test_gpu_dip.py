@@ -356,6 +356,28 @@ def test_early_stop_device_vs_reference_logic(L):
     np.testing.assert_allclose(st.best, min(ref.vars), rtol=1e-9)
 
 
+def test_early_stop_sliding_sums_over_many_windows(L):
+    """The ES window sums slide from step to step and are re-summed from the ring every 10 windows
+    (k_es_step / k_es_decide): over 700 updates -- two re-sums, the fill, the wrap -- every variance
+    the device forms matches the last 30 outputs' variance recomputed in fp64 to 1e-10."""
+    from lrspnp.dip import EarlyStopper
+    g = torch.Generator().manual_seed(11)
+    N, size = 3001, 30
+    es = EarlyStopper(N, size, 10 ** 6)
+    base = torch.rand(N, generator=g, dtype=torch.float64) * 0.8
+    hist = []
+    for i in range(700):
+        img = (base + (0.05 + 0.04 * np.sin(i / 17.0)) * torch.randn(N, generator=g, dtype=torch.float64)).float()
+        hist.append(img.double())
+        assert L.lrs_es_update_f32(P(img.cuda()), N, P(es.ring), P(es.state), None) == 0
+        if i + 1 >= size and (i % 37 == 0 or i in (size - 1, 299, 300, 599, 600, 699)):
+            st = es.read()
+            w = torch.stack(hist[-size:])
+            ref = float(((w - w.mean(0)) ** 2).sum()) / N / size
+            assert abs(st.last_var - ref) <= 1e-10 * ref, (i, st.last_var, ref)
+    assert es.read().count == 700
+
+
 def test_early_stop_device_vs_reference_golden(L, golden):
     """lrs_es_update_f32 against the reference's own get_DIP_out early stopping (EarlyStop +
     myMetric, float32 numpy; tests/golden/gen_es_golden.py) on three recorded trajectories: the
