@@ -405,6 +405,11 @@ int lrs_dipnet_train_steps(lrs_dipnet *net, const float *x, const float *target,
                            float *ring, int nsteps, int use_graph, void *stream);
 /* loss of the last step (synchronises the stream; diagnostics only) */
 int lrs_dipnet_last_loss(lrs_dipnet *net, double *loss, void *stream);
+/* Stream ordering between two streams of one device: work enqueued on `waiter` after this call runs
+ * after the work enqueued on `signaler` before it (an event with a device-scope release: cheaper
+ * than a default event when nothing on the host waits on it).  The Python side orders the DIP
+ * stream against the caller's this way. */
+int lrs_stream_wait(void *waiter, void *signaler);
 
 /* ---- Metrics (not timed) -------------------------------------------------------------------
  * acc (device double) = sum of the SSIM map of pytorch_ssim.ssim(img1, img2) over C x H x W

@@ -148,6 +148,7 @@ def _declare(L):
         "lrs_dipnet_node_buffer": (c.c_size_t, [vp, i32, i32]),
         "lrs_dipnet_train_steps": (i32, [vp, vp, vp, vp, f32, f32, f32, f32, vp, vp, i32, i32, vp]),
         "lrs_dipnet_last_loss": (i32, [vp, c.POINTER(f64), vp]),
+        "lrs_stream_wait": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -138,6 +138,20 @@ def _check(rc, what):
         raise _lib.LrsError(f"{what} failed: {_lib.LRS_E.get(rc, rc)}")
 
 
+# Orders the DIP stream against the caller's with a device-scope event (lrs_stream_wait) instead of
+# torch's wait_stream (an event with the default system-scope release); False: torch's (A/B only).
+DEVICE_SCOPE_WAITS = True
+
+
+def stream_wait(waiter, signaler):
+    """waiter's later work runs after signaler's work so far (two streams of one device)."""
+    if not DEVICE_SCOPE_WAITS:
+        waiter.wait_stream(signaler)
+        return
+    _check(_lib.device_lib().lrs_stream_wait(ctypes.c_void_p(waiter.cuda_stream), ctypes.c_void_p(signaler.cuda_stream)),
+           "lrs_stream_wait")
+
+
 class DipNet:
     """A sequential conv net on the HIP engine (lrs_dipnet_*), with flat parameter buffers."""
 
@@ -282,14 +296,14 @@ class DipNet:
         use_graph: replay one captured hipGraph per step instead of the eager launches (bit-identical,
         measured slower: DESIGN.md §5 -- off by default, as in DipConfig)."""
         import torch
-        self.stream.wait_stream(torch.cuda.current_stream())
+        stream_wait(self.stream, torch.cuda.current_stream())
         rc = self.L.lrs_dipnet_train_steps(
             self.h, _ptr(x), _ptr(target), _ptr(mask), ctypes.c_float(lr), ctypes.c_float(betas[0]),
             ctypes.c_float(betas[1]), ctypes.c_float(eps), _ptr(es.state) if es else None,
             _ptr(es.ring) if es else None, int(nsteps), 1 if use_graph else 0,
             ctypes.c_void_p(self.stream.cuda_stream))
         _check(rc, "lrs_dipnet_train_steps")
-        torch.cuda.current_stream().wait_stream(self.stream)
+        stream_wait(torch.cuda.current_stream(), self.stream)
 
     def node_buffer(self, node: int, which: int = 0):
         """A copy of node `node`'s workspace buffer (0 output, 1 pre-BN z, 2 dL/dz, 3 dL/d(output);
@@ -388,7 +402,7 @@ class DipProx:
         cfg = self.cfg
         n_iter = cfg.num_iter if num_iter is None else num_iter
         net = self.net
-        net.stream.wait_stream(torch.cuda.current_stream())
+        stream_wait(net.stream, torch.cuda.current_stream())
         net.init_params(self.calls if seed is None else seed)
         self.calls += 1
         if not early_stop:
@@ -407,7 +421,7 @@ class DipProx:
             st = self.es.read(net.stream)
             if st.stop:
                 break
-        torch.cuda.current_stream().wait_stream(net.stream)
+        stream_wait(torch.cuda.current_stream(), net.stream)
         self.last_steps = done
         if st is not None and st.stop:
             self.last_stop_epoch = st.stop_epoch

@@ -18,6 +18,7 @@ import torch
 
 from . import ops
 from ._lib import LrsError
+from .dip import stream_wait
 
 
 @dataclass
@@ -279,7 +280,7 @@ class LrsPnP:
         main = torch.cuda.current_stream()
         lr = self.lowrank_stream
         warm = self.cfg.svt_warm and self.iteration > 0
-        lr.wait_stream(main)
+        stream_wait(lr, main)
         # low-rank prox, first half (whole chip, ~0.2 ms): fp64 Gram (+ Jacobi warm-start products)
         ops.svt_gram(self.X, self.L2, self.c2, self.svt_ws, warm=warm, stream=lr, method=self.cfg.svt_method)
         if self.comm is not None:
@@ -299,7 +300,7 @@ class LrsPnP:
             # its Gram waits for the first sparse-coding workgroups to retire
             main.wait_event(gram_done)
         self._ista(self.cfg.Nit, main)
-        main.wait_stream(lr)
+        stream_wait(main, lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
                         self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)
         self.iteration += 1
@@ -307,7 +308,7 @@ class LrsPnP:
     def _step_dip(self):
         main = torch.cuda.current_stream()
         lr = self.lowrank_stream
-        lr.wait_stream(main)
+        stream_wait(lr, main)
         # sparse coding is enqueued first so it runs beside the DIP training
         ops.im2col(self.X, self.L1, self.mu1_32, self.cfg.bb, self.rows_d, self.cols_d, self.n_pad, Yb=self.Yb,
                    stream=main)
@@ -325,11 +326,11 @@ class LrsPnP:
                            max_workgroups=self.cfg.ista_max_wg_dip)
                 done += it
         if self.cfg.ista_dip_order == "before":
-            lr.wait_stream(main)
+            stream_wait(lr, main)
         elif self.cfg.ista_dip_order != "beside":
             raise LrsError(f"unknown ista_dip_order {self.cfg.ista_dip_order!r} (beside | before)")
         self.low_rank_dip(lr)
-        main.wait_stream(lr)
+        stream_wait(main, lr)
         ops.admm_update(self.X, self.L1, self.L2, self.Y, self.M, self.U, self.phi, self.cfg.bb, self.grid,
                         self.gamma32, self.mu1_32, self.mu2_32, norms=self.norms, stream=main)
         self.iteration += 1

@@ -356,6 +356,24 @@ def test_early_stop_device_vs_reference_logic(L):
     np.testing.assert_allclose(st.best, min(ref.vars), rtol=1e-9)
 
 
+def test_stream_wait_orders_streams(L):
+    """lrs_stream_wait (dip.stream_wait, the DIP stream's ordering against the caller's): work enqueued
+    on the waiter after the call sees the signaller's earlier writes, even behind a long kernel."""
+    from lrspnp.dip import stream_wait
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    x = torch.zeros(1 << 22, device="cuda")
+    for v in (3.0, 5.0):
+        with torch.cuda.stream(a):
+            torch.cuda._sleep(20_000_000)      # ~10 ms of spinning before the write
+            x.fill_(v)
+        stream_wait(b, a)
+        with torch.cuda.stream(b):
+            y = x * 2.0
+        b.synchronize()
+        assert bool((y == 2.0 * v).all())
+    torch.cuda.synchronize()
+
+
 def test_early_stop_sliding_sums_over_many_windows(L):
     """The ES window sums slide from step to step and are re-summed from the ring every 10 windows
     (k_es_step / k_es_decide): over 700 updates -- two re-sums, the fill, the wrap -- every variance
