@@ -364,7 +364,11 @@ class DipConfig:
     learning_rate: float = 0.1
     es_size: int = 30
     patience: int = 60
-    poll_every: int = 10          # host polls the device ES flag every this many steps (< es_size)
+    # host polls of the device ES state: None = after exactly the steps until the earliest epoch at
+    # which the rule could stop (es_size - count + patience while filling, else patience - wait): a
+    # stop always falls on a batch's last step, so no step runs past it and polls are few; an int =
+    # every this many steps (< es_size, so the stop epoch's ring slot survives the overshoot)
+    poll_every: int | None = None
     use_graph: bool = False       # replay one captured hipGraph per step (measured slower than
                                   # direct launches on ROCm 7.2 for this ~110-kernel step)
     hidden: int = 128
@@ -415,7 +419,7 @@ class DipProx:
         done = 0
         st = None
         while done < n_iter:
-            k = min(cfg.poll_every, n_iter - done)
+            k = min(cfg.poll_every or self.steps_to_possible_stop(st), n_iter - done)
             net.train_steps(dip_input, target, mask, k, cfg.learning_rate, es=self.es, use_graph=cfg.use_graph)
             done += k
             st = self.es.read(net.stream)
@@ -429,6 +433,18 @@ class DipProx:
         # the reference returns None here (its loop ends without returning); use the last output
         self.last_stop_epoch = None
         return self.es.slot_of(st.count - 1).view(net.out_shape)
+
+
+    def steps_to_possible_stop(self, st) -> int:
+        """Training steps until the earliest epoch at which EarlyStop could stop, from the state after
+        the last poll (None: before the first step).  While the window fills no test runs; the first
+        test always improves on best = inf (wait = 0); after it, wait grows by at most one per step and
+        the rule stops when it reaches patience (…1-LiP.py:71-99)."""
+        size, patience = self.cfg.es_size, self.cfg.patience
+        count = 0 if st is None else st.count
+        if count < size:
+            return size - count + patience
+        return max(1, patience - st.wait)
 
 
 LipschitzDip = DipProx   # the 1-Lip name used by the first callers

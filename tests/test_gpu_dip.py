@@ -694,6 +694,26 @@ def test_lipschitz_dip_run_early_stop(L):
     assert torch.isfinite(out2).all()
 
 
+def test_lipschitz_dip_adaptive_polls_equal_every_step(L):
+    """DipConfig.poll_every=None (polls after the steps until the earliest possible stop) against a poll
+    after every step: the same stop epoch, no step past it, the same returned output bit for bit; the
+    fixed 10-step cadence stops at the same epoch too (with up to 9 steps past it)."""
+    from lrspnp.dip import DipConfig, LipschitzDip
+    units, flat, x, t, m = _problem()
+    args = (t.cuda(), x.cuda(), m.reshape(-1).cuda())
+    res = {}
+    for pe in (None, 1, 10):
+        dip = LipschitzDip(128, 36, 36, DipConfig(num_iter=600, poll_every=pe))
+        out = dip.run(*args, seed=5)
+        torch.cuda.synchronize()
+        res[pe] = (dip.last_stop_epoch, dip.last_steps, out.clone())
+    stop, steps, out = res[None]
+    assert stop is not None and stop >= 89
+    assert steps == stop + 1 and res[1][1] == stop + 1
+    assert res[1][0] == stop and res[10][0] == stop
+    assert torch.equal(out, res[1][2]) and torch.equal(out, res[10][2])
+
+
 def test_layout_transforms_match_reference_reshapes(L):
     from lrspnp import ops
     g = np.random.default_rng(0)
